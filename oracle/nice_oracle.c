@@ -1,0 +1,784 @@
+/*
+ * nice_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded restatement of the reference NICE2 codec
+ * (wouter-rombouts/fast-losless-image-compression-format, Rust, release profile)
+ * used as the CHECKER for the MI355X HIP path and as the timed CPU baseline
+ * ("kind": "port") in bench.py.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library.  The product library
+ * (libnice_hip.so) never links, loads or calls it.
+ *
+ * Parity pinning: the reference is Rust and no Rust toolchain exists in this
+ * image, so it cannot be built or run here.  This restatement is
+ * pinned by (1) the reference's own known-answer tests (bitwriter.rs:86-97,
+ * bitreader.rs:106-146, hfe.rs:300-348 round trip), ported in
+ * tests/test_oracle_kat.py, and (2) byte sizes / max code lengths produced by a
+ * second, independent restatement during the survey.
+ * Full-stream byte parity against the Rust binary is therefore "unpinned" by
+ * reference outputs; see DESIGN.md §Parity.
+ *
+ * Rust release semantics reproduced (Cargo.toml:12-16): wrapping +/- on
+ * u8/u32/usize, shift amounts masked to the operand width, `u8::next_power_of_two`
+ * wrapping to 0 above 128, `io::Read` on an exhausted slice returning Ok(0)
+ * (stale buffer byte reused, bitreader.rs:90-96), std `BinaryHeap` push/pop
+ * order (hfe.rs:63-84 with the reversed Ord of hfe.rs:246-251).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "nice_oracle.h"
+
+/* ------------------------------------------------------------------------- */
+/* Format constants: code.rs:16-45 (prefix ids, stream ids), code.rs:91-116   */
+/* (alphabet sizes, in stream order).                                         */
+/* ------------------------------------------------------------------------- */
+enum {
+    P_BACK_REF = 0, P_RGB = 1, P_LUMA = 2, P_SMALL_DIFF = 3, P_LUMA2 = 4, P_RUN1 = 5
+};
+enum {
+    S_RGB = 0, S_PREFIX = 1, S_LUMA_BASE = 2, S_LUMA_OTHER = 3, S_LUMA_REF = 4,
+    S_SMALL_DIFF = 5, S_LUMA2_BASE = 6, S_LUMA2_R = 7, S_LUMA2_B = 8, S_BACK_REF = 9,
+    N_STREAMS = 10
+};
+static const int STREAM_N[N_STREAMS] = {256, 13, 64, 32, 11, 343, 64, 32, 32, 11};
+
+/* ------------------------------------------------------------------------- */
+/* Growable byte sink (stands in for the Vec<u8>/io::Write of main.rs:61).    */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint8_t *p; size_t len, cap; int oom; } sink_t;
+
+static void sink_put(sink_t *s, uint8_t b) {
+    if (s->len == s->cap) {
+        size_t nc = s->cap ? s->cap * 2 : 4096;
+        uint8_t *np = (uint8_t *)realloc(s->p, nc);
+        if (!np) { s->oom = 1; return; }
+        s->p = np; s->cap = nc;
+    }
+    s->p[s->len++] = b;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Bitwriter: bitwriter.rs:3-73.  bit_offset is u8, cache is u32.             */
+/* ------------------------------------------------------------------------- */
+typedef struct { sink_t *w; uint8_t bit_offset; uint32_t cache; } bitwriter_t;
+
+static inline uint32_t shl32(uint32_t v, unsigned s) { return v << (s & 31u); }
+static inline uint32_t shr32(uint32_t v, unsigned s) { return v >> (s & 31u); }
+
+/* bitwriter.rs:17-35 -- at most one byte flushed per call. */
+static void bw_write_8bits(bitwriter_t *b, uint8_t amount, uint8_t value) {
+    b->bit_offset = (uint8_t)(b->bit_offset + amount);
+    b->cache += shl32((uint32_t)value, (uint8_t)(32 - b->bit_offset));
+    if (b->bit_offset >= 8) {
+        sink_put(b->w, (uint8_t)(b->cache >> 24));
+        b->bit_offset = (uint8_t)(b->bit_offset - 8);
+        b->cache <<= 8;
+    }
+}
+
+/* bitwriter.rs:55-73 -- flushes while >= 8 bits are pending. */
+static void bw_write_24bits(bitwriter_t *b, uint8_t amount, uint32_t value) {
+    b->bit_offset = (uint8_t)(b->bit_offset + amount);
+    b->cache += shl32(value, (uint8_t)(32 - b->bit_offset));
+    while (b->bit_offset >= 8) {
+        sink_put(b->w, (uint8_t)(b->cache >> 24));
+        b->bit_offset = (uint8_t)(b->bit_offset - 8);
+        b->cache <<= 8;
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Bitreader over a byte slice: bitreader.rs:3-100.                           */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t *p; size_t len, pos;
+    uint8_t bit_offset; uint32_t cache; uint8_t buffer;
+} bitreader_t;
+
+static void br_init(bitreader_t *r, const uint8_t *p, size_t len, size_t pos) {
+    r->p = p; r->len = len; r->pos = pos; r->bit_offset = 32; r->cache = 0; r->buffer = 0;
+}
+
+/* bitreader.rs:31-54: read_exact of one byte (EOF -> Err -> the caller's
+ * unwrap panics), then extract. Returns -1 on EOF. */
+static int br_read_bitsu8(bitreader_t *r, uint8_t amount, uint8_t *out) {
+    if (amount > (uint8_t)(32 - r->bit_offset)) {
+        if (r->pos >= r->len) return -1;
+        uint8_t byte = r->p[r->pos++];
+        r->cache = (uint32_t)byte + shl32(r->cache, 8);
+        r->bit_offset = (uint8_t)(r->bit_offset - 8);
+    }
+    uint32_t ret = shr32(shl32(r->cache, r->bit_offset), (uint8_t)(32 - amount));
+    if (ret > 255) return -2;               /* try_into::<u8>().unwrap() panics */
+    r->bit_offset = (uint8_t)(r->bit_offset + amount);
+    *out = (uint8_t)ret;
+    return 0;
+}
+
+/* bitreader.rs:56-75 (test-only helper, ported for the KAT). */
+static uint32_t br_read_24bits(bitreader_t *r, uint8_t amount) {
+    uint8_t aob_rev = (uint8_t)(32 - amount);
+    while (r->bit_offset > aob_rev) {
+        if (r->pos < r->len) r->buffer = r->p[r->pos++];   /* read_exact().expect() */
+        r->bit_offset = (uint8_t)(r->bit_offset - 8);
+        r->cache = (uint32_t)r->buffer + shl32(r->cache, 8);
+    }
+    r->bit_offset = (uint8_t)(r->bit_offset + amount);
+    return shr32(shl32(r->cache, (uint8_t)(r->bit_offset - amount)), aob_rev);
+}
+
+/* bitreader.rs:78-100: `Read::read` on an exhausted slice returns Ok(0) and
+ * leaves `buffer` holding the previous byte, which is shifted in again. */
+static uint32_t br_read_24bits_noclear(bitreader_t *r, uint8_t amount) {
+    uint8_t aob_rev = (uint8_t)(32 - amount);
+    while (r->bit_offset > aob_rev) {
+        if (r->pos < r->len) r->buffer = r->p[r->pos++];
+        r->bit_offset = (uint8_t)(r->bit_offset - 8);
+        r->cache = shl32(r->cache, 8) + (uint32_t)r->buffer;
+    }
+    return shr32(shl32(r->cache, r->bit_offset), aob_rev);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Huffman code lengths: hfe.rs:58-87 with std BinaryHeap<TreeNode>.           */
+/* TreeNode's Ord is reversed on occurrences_sum (hfe.rs:246-251), so the     */
+/* max-heap behaves as a min-heap on counts.  Only counts are compared.        */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint64_t cnt; int32_t node; } hn_t;
+
+/* std BinaryHeap::sift_up(start, pos): move up while elem < parent in the
+ * reversed order, i.e. while elem.cnt < parent.cnt. */
+static size_t heap_sift_up(hn_t *d, size_t start, size_t pos) {
+    hn_t e = d[pos];
+    while (pos > start) {
+        size_t parent = (pos - 1) / 2;
+        if (d[parent].cnt <= e.cnt) break;            /* elem <= parent */
+        d[pos] = d[parent];
+        pos = parent;
+    }
+    d[pos] = e;
+    return pos;
+}
+
+/* std BinaryHeap::sift_down_to_bottom(pos): walk to the bottom always taking
+ * the "greater" child (right iff right.cnt <= left.cnt), then sift_up. */
+static void heap_sift_down_to_bottom(hn_t *d, size_t len, size_t pos) {
+    size_t end = len, start = pos;
+    hn_t e = d[pos];
+    size_t child = 2 * pos + 1;
+    size_t lim = end >= 2 ? end - 2 : 0;
+    while (child <= lim && end >= 2) {
+        if (d[child + 1].cnt <= d[child].cnt) child += 1;
+        d[pos] = d[child];
+        pos = child;
+        child = 2 * pos + 1;
+    }
+    if (child == end - 1) {
+        d[pos] = d[child];
+        pos = child;
+    }
+    d[pos] = e;
+    heap_sift_up(d, start, pos);
+}
+
+static void heap_push(hn_t *d, size_t *len, hn_t x) {
+    d[*len] = x;
+    *len += 1;
+    heap_sift_up(d, 0, *len - 1);
+}
+
+static hn_t heap_pop(hn_t *d, size_t *len) {
+    *len -= 1;
+    hn_t item = d[*len];
+    if (*len > 0) {
+        hn_t t = d[0]; d[0] = item; item = t;
+        heap_sift_down_to_bottom(d, *len, 0);
+    }
+    return item;
+}
+
+/* Code lengths for one stream (hfe.rs:62-84).  aob starts at 1 and every merge
+ * adds 1 (u8, wrapping) to each symbol under the merged node; the loop stops
+ * with two nodes left.  We keep parent links instead of concatenated symbol
+ * vectors: aob(sym) = 1 + (#merged ancestors of sym).  Exposed for tests. */
+void nice_oracle_code_lengths(const uint64_t *counts, int n, uint8_t *aob) {
+    hn_t *heap = (hn_t *)malloc(sizeof(hn_t) * (size_t)(n + 1));
+    int32_t *parent = (int32_t *)malloc(sizeof(int32_t) * (size_t)(2 * n + 2));
+    size_t len = 0;
+    int next = n;
+    for (int i = 0; i < 2 * n + 2; ++i) parent[i] = -1;
+    for (int i = 0; i < n; ++i) {
+        hn_t x = {counts[i], i};
+        heap_push(heap, &len, x);
+    }
+    while (len > 2) {
+        hn_t a = heap_pop(heap, &len);
+        hn_t b = heap_pop(heap, &len);
+        int id = next++;
+        parent[a.node] = id;
+        parent[b.node] = id;
+        hn_t m = {a.cnt + b.cnt, id};
+        heap_push(heap, &len, m);
+    }
+    for (int i = 0; i < n; ++i) {
+        unsigned depth = 0;
+        for (int p = parent[i]; p >= 0; p = parent[p]) depth++;
+        aob[i] = (uint8_t)(1u + depth);
+    }
+    free(heap);
+    free(parent);
+}
+
+/* amount_of_bits_to_bcodes: hfe.rs:255-296.  Sort by (aob desc, symbol desc),
+ * walk with a usize running code.  Exposed for tests. */
+typedef struct { int sym; uint8_t aob; } so_t;
+static int so_cmp(const void *pa, const void *pb) {
+    const so_t *a = (const so_t *)pa, *b = (const so_t *)pb;
+    if (a->aob != b->aob) return a->aob > b->aob ? -1 : 1;
+    return a->sym > b->sym ? -1 : (a->sym < b->sym ? 1 : 0);
+}
+void nice_oracle_canonical(const uint8_t *aob, int n, uint64_t *code) {
+    so_t *s = (so_t *)malloc(sizeof(so_t) * (size_t)n);
+    for (int i = 0; i < n; ++i) { s[i].sym = i; s[i].aob = aob[i]; }
+    qsort(s, (size_t)n, sizeof(so_t), so_cmp);
+    uint64_t cur = 0;
+    uint8_t prev = 0;
+    for (int k = 0; k < n; ++k) {
+        uint8_t a = s[k].aob;
+        if (a < prev) cur >>= ((uint8_t)(prev - a)) & 63u;
+        if (prev > 0) cur += 1;
+        code[s[k].sym] = (((uint64_t)1) << (a & 63u)) - cur - 1;
+        prev = a;
+    }
+    free(s);
+}
+
+/* u8::next_power_of_two().count_zeros() in release mode (hfe.rs:102,178). */
+static uint8_t field_bits(uint8_t max_aob) {
+    unsigned np;
+    if (max_aob <= 1) np = 1;
+    else if (max_aob > 128) np = 0;               /* wraps to 0 */
+    else { np = 1; while (np < max_aob) np <<= 1; }
+    unsigned pop = 0;
+    for (unsigned b = np; b; b >>= 1) pop += b & 1u;
+    return (uint8_t)(8 - pop);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Encoder: code.rs:59-457 + hfe.rs:29-117.                                    */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint16_t sym; uint8_t stream; } symrec_t;
+typedef struct {
+    symrec_t *v; size_t len, cap; int oom;
+    uint64_t *occ[N_STREAMS];
+} encout_t;
+
+static void add_symbol(encout_t *e, unsigned sym, int stream) {
+    if (e->len == e->cap) {
+        size_t nc = e->cap ? e->cap * 2 : 4096;
+        symrec_t *np = (symrec_t *)realloc(e->v, nc * sizeof(symrec_t));
+        if (!np) { e->oom = 1; return; }
+        e->v = np; e->cap = nc;
+    }
+    e->v[e->len].sym = (uint16_t)sym;
+    e->v[e->len].stream = (uint8_t)stream;
+    e->len++;
+    e->occ[stream][sym] += 1;
+}
+
+/* Pixel RGB at byte position pos (channels bytes per pixel; only +0..+2 read). */
+static inline int rgb_eq(const uint8_t *in, size_t a, size_t b) {
+    return in[a] == in[b] && in[a + 1] == in[b + 1] && in[a + 2] == in[b + 2];
+}
+
+int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+                       uint8_t channels, uint8_t channels_out,
+                       uint8_t **out, size_t *out_len, nice_oracle_stats *stats) {
+    *out = NULL; *out_len = 0;
+    if (channels < 3) return NICE_ORACLE_E_ARG;
+    const size_t W = width, ch = channels;
+    const size_t image_size = (size_t)height * W * ch;                 /* code.rs:85 */
+    if (in_len < image_size) return NICE_ORACLE_E_ARG;
+    sink_t sink = {0};
+    /* header: code.rs:72-84 */
+    sink_put(&sink, 'n'); sink_put(&sink, 'i'); sink_put(&sink, 'c'); sink_put(&sink, 'e');
+    for (int s = 24; s >= 0; s -= 8) sink_put(&sink, (uint8_t)(width >> s));
+    for (int s = 24; s >= 0; s -= 8) sink_put(&sink, (uint8_t)(height >> s));
+    sink_put(&sink, channels_out);
+
+    encout_t e = {0};
+    for (int s = 0; s < N_STREAMS; ++s) e.occ[s] = (uint64_t *)calloc((size_t)STREAM_N[s], 8);
+
+    /* ref tables: code.rs:141-145 (usize wrapping arithmetic) */
+    const size_t rel_ref[11] = {ch, ch * W, ch * (W - 1), ch * (W - 3), 3 * ch,
+                                ch * (3 * W - 1), 3 * ch * W, ch * (3 * W + 1), ch * (W + 3),
+                                ch * 3 * (W + 1), ch * 3 * (W - 1)};
+    const size_t back_ref[5] = {ch, ch * W, ch * (W - 1), 2 * ch, 2 * ch * W};
+    const size_t rowb = ch * W;
+
+    size_t position = 0, prev_position = 0;
+    uint64_t n_coded = 0, n_br = 0, n_sd = 0, n_l2 = 0, n_luma = 0, n_rgb = 0, n_runpx = 0;
+    while (position < image_size) {                                      /* code.rs:159 */
+        n_coded++;
+        int done = 0;
+        /* back references: code.rs:191-206 */
+        for (int k = 0; k < 5 && !done; ++k) {
+            if (position >= back_ref[k]) {
+                size_t rp = position - back_ref[k];
+                if (rgb_eq(in, position, rp)) {
+                    add_symbol(&e, P_BACK_REF, S_PREFIX);
+                    add_symbol(&e, (unsigned)k, S_BACK_REF);
+                    done = 1; n_br++;
+                }
+            }
+        }
+        if (!done) {
+            /* small diff: code.rs:208-247 (i16 arithmetic) */
+            int d[3];
+            for (int c = 0; c < 3; ++c)
+                d[c] = (int)in[position + c] - (int)in[prev_position + c];
+            if (position >= rowb) {
+                for (int c = 0; c < 3; ++c)
+                    d[c] = (int)in[position + c] -
+                           ((int)in[position - rowb + c] + (int)in[prev_position + c]) / 2;
+            }
+            if (position > 0 && d[0] >= -3 && d[0] <= 3 && d[1] >= -3 && d[1] <= 3 &&
+                d[2] >= -3 && d[2] <= 3) {
+                add_symbol(&e, P_SMALL_DIFF, S_PREFIX);
+                unsigned code = (unsigned)(3 + d[0]) + 7u * (unsigned)(3 + d[1]) +
+                                49u * (unsigned)(3 + d[2]);
+                add_symbol(&e, code, S_SMALL_DIFF);
+                done = 1; n_sd++;
+            }
+        }
+        if (!done && position >= rowb) {
+            /* luma2: code.rs:252-292 (u8 wrapping arithmetic) */
+            size_t rp = position - rowb;
+            uint8_t a[3];
+            for (int c = 0; c < 3; ++c)
+                a[c] = (uint8_t)(((unsigned)in[rp + c] + (unsigned)in[prev_position + c]) / 2);
+            uint8_t g = (uint8_t)(in[position + 1] - a[1]);
+            uint8_t r = (uint8_t)((uint8_t)(in[position] - a[0]) - g);
+            uint8_t b = (uint8_t)((uint8_t)(in[position + 2] - a[2]) - g);
+            if (position > 0 && (g >= 224 || g < 32) && (r >= 240 || r < 16) &&
+                (b >= 240 || b < 16)) {
+                add_symbol(&e, P_LUMA2, S_PREFIX);
+                add_symbol(&e, (uint8_t)(g + 32), S_LUMA2_BASE);
+                add_symbol(&e, (uint8_t)(r + 16), S_LUMA2_R);
+                add_symbol(&e, (uint8_t)(b + 16), S_LUMA2_B);
+                done = 1; n_l2++;
+            }
+        }
+        if (!done) {
+            /* luma with relative refs: code.rs:293-339 */
+            for (int k = 0; k < 11 && !done; ++k) {
+                if (position >= rel_ref[k]) {
+                    size_t rp = position - rel_ref[k];
+                    uint8_t g = (uint8_t)(in[position + 1] - in[rp + 1]);
+                    uint8_t r = (uint8_t)((uint8_t)(in[position] - in[rp]) - g);
+                    uint8_t b = (uint8_t)((uint8_t)(in[position + 2] - in[rp + 2]) - g);
+                    if (position > 0 && (g >= 224 || g < 32) && (r >= 240 || r < 16) &&
+                        (b >= 240 || b < 16)) {
+                        add_symbol(&e, P_LUMA, S_PREFIX);
+                        add_symbol(&e, (unsigned)k, S_LUMA_REF);
+                        add_symbol(&e, (uint8_t)(g + 32), S_LUMA_BASE);
+                        add_symbol(&e, (uint8_t)(r + 16), S_LUMA_OTHER);
+                        add_symbol(&e, (uint8_t)(b + 16), S_LUMA_OTHER);
+                        done = 1; n_luma++;
+                    }
+                }
+            }
+        }
+        if (!done) {
+            /* rgb: code.rs:341-366 */
+            add_symbol(&e, P_RGB, S_PREFIX);
+            for (int c = 0; c < 3; ++c) {
+                uint8_t v = (uint8_t)(in[position + c] - (position > 0 ? in[prev_position + c] : 0));
+                if (position >= rowb)
+                    v = (uint8_t)((int)in[position + c] -
+                                  ((int)in[position - rowb + c] + (int)in[prev_position + c]) / 2);
+                add_symbol(&e, v, S_RGB);
+            }
+            n_rgb++;
+        }
+        /* run: code.rs:371-407 */
+        size_t run_length = 0, rlp = position + ch;
+        while (rlp < image_size && rgb_eq(in, rlp, position)) { run_length++; rlp += ch; }
+        if (run_length > 0) {
+            n_runpx += run_length;
+            position += run_length * ch;
+            run_length -= 1;
+            for (;;) {
+                add_symbol(&e, (unsigned)(run_length % 8 + 5), S_PREFIX);
+                if (run_length < 8) break;
+                run_length /= 8;
+            }
+        }
+        prev_position = position;                                           /* code.rs:412 */
+        position += ch;
+    }
+
+    /* to_encoded_output: hfe.rs:51-117 */
+    bitwriter_t bw = {&sink, 0, 0};
+    uint8_t *aob[N_STREAMS];
+    uint64_t *code[N_STREAMS];
+    for (int s = 0; s < N_STREAMS; ++s) {
+        int n = STREAM_N[s];
+        aob[s] = (uint8_t *)malloc((size_t)n);
+        code[s] = (uint64_t *)malloc(8 * (size_t)n);
+        nice_oracle_code_lengths(e.occ[s], n, aob[s]);
+        nice_oracle_canonical(aob[s], n, code[s]);
+        uint8_t mx = 0;
+        for (int i = 0; i < n; ++i) if (aob[s][i] > mx) mx = aob[s][i];
+        if (stats) stats->max_aob[s] = mx;
+        bw_write_8bits(&bw, 5, mx);                                     /* hfe.rs:98 */
+        uint8_t fb = field_bits(mx);
+        for (int i = 0; i < n; ++i) bw_write_8bits(&bw, fb, aob[s][i]); /* hfe.rs:100-103 */
+    }
+    size_t header_bytes = sink.len;
+    uint8_t max_emit = 0;
+    for (size_t k = 0; k < e.len; ++k) {                                /* hfe.rs:110-113 */
+        int s = e.v[k].stream, sym = e.v[k].sym;
+        if (aob[s][sym] > max_emit) max_emit = aob[s][sym];
+        bw_write_24bits(&bw, aob[s][sym], (uint32_t)code[s][sym]);
+    }
+    sink_put(&sink, (uint8_t)(bw.cache >> 24));                           /* hfe.rs:115 */
+    for (int s = 24; s >= 0; s -= 8) sink_put(&sink, (uint8_t)(bw.cache >> s)); /* code.rs:421-422 */
+
+    if (stats) {
+        stats->n_symbols = e.len;
+        stats->n_coded = n_coded; stats->n_backref = n_br; stats->n_smalldiff = n_sd;
+        stats->n_luma2 = n_l2; stats->n_luma = n_luma; stats->n_rgb = n_rgb;
+        stats->n_run_pixels = n_runpx;
+        stats->header_end = header_bytes;
+        stats->max_emitted_aob = max_emit;
+        int bin = 0;
+        for (int s = 0; s < N_STREAMS; ++s)
+            for (int i = 0; i < STREAM_N[s]; ++i, ++bin) {
+                stats->hist[bin] = e.occ[s][i];
+                stats->aob[bin] = aob[s][i];
+                stats->hist_total += e.occ[s][i];
+            }
+    }
+    int oom = sink.oom || e.oom;
+    for (int s = 0; s < N_STREAMS; ++s) { free(aob[s]); free(code[s]); free(e.occ[s]); }
+    free(e.v);
+    if (oom) { free(sink.p); return NICE_ORACLE_E_OOM; }
+    *out = sink.p;
+    *out_len = sink.len;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Decoder: code.rs:464-687 + hfe.rs:173-222.                                  */
+/* mode NICE_ORACLE_DEC_REFERENCE follows the reference literally: pixel       */
+/* stride 3 after coded pixels (code.rs:659) and `channels` elsewhere; every   */
+/* Rust panic (index out of bounds, read_exact EOF, over-long shift in the LUT */
+/* fill) becomes an error code.  NICE_ORACLE_DEC_STRIDE uses `channels` as the */
+/* stride everywhere (the evident intent), used only to check RGBA round trips.*/
+/* ------------------------------------------------------------------------- */
+typedef struct { uint16_t symbol; uint8_t aob; } lut_t;
+typedef struct { uint8_t max_aob; lut_t *lut; size_t lut_len; } sslookup_t;
+
+static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
+    uint8_t mx;
+    if (br_read_bitsu8(r, 5, &mx)) return NICE_ORACLE_E_PANIC;
+    sl->max_aob = mx;
+    uint8_t fb = field_bits(mx);
+    uint8_t *a = (uint8_t *)malloc((size_t)n);
+    uint64_t *code = (uint64_t *)malloc(8 * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        if (br_read_bitsu8(r, fb, &a[i])) { free(a); free(code); return NICE_ORACLE_E_PANIC; }
+    }
+    nice_oracle_canonical(a, n, code);
+    sl->lut_len = (size_t)1 << (mx & 63u);
+    sl->lut = (lut_t *)calloc(sl->lut_len, sizeof(lut_t));
+    int rc = 0;
+    for (int i = 0; i < n && !rc; ++i) {
+        unsigned sh = ((uint8_t)(mx - a[i])) & 63u;
+        uint64_t lo = code[i] << sh, hi = (code[i] + 1) << sh;
+        for (uint64_t k = lo; k < hi; ++k) {
+            if (k >= sl->lut_len) { rc = NICE_ORACLE_E_PANIC; break; }
+            sl->lut[k].symbol = (uint16_t)i;
+            sl->lut[k].aob = a[i];
+        }
+    }
+    free(a); free(code);
+    return rc;
+}
+
+static inline int read_next_symbol(bitreader_t *r, const sslookup_t *sl, unsigned *sym) {
+    uint32_t v = br_read_24bits_noclear(r, sl->max_aob);
+    if (v >= sl->lut_len) return NICE_ORACLE_E_PANIC;
+    lut_t l = sl->lut[v];
+    r->bit_offset = (uint8_t)(r->bit_offset + l.aob);
+    *sym = l.symbol;
+    return 0;
+}
+
+int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, size_t *out_len,
+                       uint32_t *w_out, uint32_t *h_out, uint8_t *ch_out) {
+    *out = NULL; *out_len = 0;
+    /* header: code.rs:469-483 (io::Read::read on a slice, magic not checked) */
+    size_t pos = 0;
+    uint8_t hb[13] = {0};
+    {
+        size_t take = len < 4 ? len : 4; pos += take;                   /* magic */
+        uint8_t buf[4] = {0};
+        for (int f = 0; f < 2; ++f) {
+            size_t t = len - pos < 4 ? len - pos : 4;
+            memcpy(buf, s + pos, t); pos += t;                         /* short read keeps old bytes */
+            memcpy(hb + 4 + 4 * f, buf, 4);
+        }
+        uint8_t cb[1] = {0};
+        if (pos < len) cb[0] = s[pos++];
+        hb[12] = cb[0];
+    }
+    uint32_t width = ((uint32_t)hb[4] << 24) | ((uint32_t)hb[5] << 16) | ((uint32_t)hb[6] << 8) | hb[7];
+    uint32_t height = ((uint32_t)hb[8] << 24) | ((uint32_t)hb[9] << 16) | ((uint32_t)hb[10] << 8) | hb[11];
+    size_t ch = hb[12];
+    *w_out = width; *h_out = height; *ch_out = (uint8_t)ch;
+    const size_t W = width;
+    const size_t image_size = W * (size_t)height * ch;
+    uint8_t *o = (uint8_t *)calloc(image_size ? image_size : 1, 1);   /* see DESIGN.md: set_len */
+    if (!o) return NICE_ORACLE_E_OOM;
+    bitreader_t r;
+    br_init(&r, s, len, pos);
+    sslookup_t L[N_STREAMS];
+    memset(L, 0, sizeof(L));
+    int rc = 0;
+    for (int k = 0; k < N_STREAMS && !rc; ++k) rc = read_header_into_tree(&r, &L[k], STREAM_N[k]);
+    const size_t rel_ref[11] = {ch, ch * W, ch * (W - 1), ch * (W - 3), 3 * ch,
+                                ch * (3 * W - 1), 3 * ch * W, ch * (3 * W + 1), ch * (W + 3),
+                                ch * 3 * (W + 1), ch * 3 * (W - 1)};
+    const size_t back_ref[5] = {ch, ch * W, ch * (W - 1), 2 * ch, 2 * ch * W};
+    const size_t rowb = ch * W;
+    const size_t step = (mode == NICE_ORACLE_DEC_STRIDE) ? ch : 3;     /* code.rs:659 */
+    unsigned prefix = 0, v;
+#define RS(stream, dst) do { if (read_next_symbol(&r, &L[stream], &(dst))) { rc = NICE_ORACLE_E_PANIC; goto done; } } while (0)
+#define IDX(i) do { if ((i) >= image_size) { rc = NICE_ORACLE_E_PANIC; goto done; } } while (0)
+    if (rc) goto done;
+    RS(S_PREFIX, prefix);                                               /* code.rs:550 */
+    size_t position = 0, prev_pos = 0;
+    while (position < image_size) {                                      /* code.rs:573 */
+        switch (prefix) {
+        case P_LUMA2: {                                                  /* code.rs:579-588 */
+            unsigned gs, rs2, bs;
+            RS(S_LUMA2_BASE, gs);
+            uint8_t g = (uint8_t)(gs - 32);
+            size_t up = position - rowb;
+            IDX(position + 2); IDX(prev_pos + 2); IDX(up + 2);
+            o[position + 1] = (uint8_t)(g + (uint8_t)(((unsigned)o[prev_pos + 1] + o[up + 1]) / 2));
+            RS(S_LUMA2_R, rs2);
+            o[position] = (uint8_t)((uint8_t)(rs2 - 16) + (uint8_t)(g + (uint8_t)(((unsigned)o[prev_pos] + o[up]) / 2)));
+            RS(S_LUMA2_B, bs);
+            o[position + 2] = (uint8_t)((uint8_t)(bs - 16) + (uint8_t)(g + (uint8_t)(((unsigned)o[prev_pos + 2] + o[up + 2]) / 2)));
+            break;
+        }
+        case P_SMALL_DIFF: {                                             /* code.rs:589-618 */
+            unsigned sd;
+            RS(S_SMALL_DIFF, sd);
+            int sdi = (int)(int16_t)sd;
+            int rd = sdi % 7; sdi = (sdi - rd) / 7;
+            int gd = sdi % 7; int bd = (sdi - gd) / 7;
+            int rr, rg, rb;
+            IDX(position + 2); IDX(prev_pos + 2);
+            if (position >= rowb) {
+                size_t vp = position - rowb;
+                rr = ((int)o[vp] + o[prev_pos]) / 2;
+                rg = ((int)o[vp + 1] + o[prev_pos + 1]) / 2;
+                rb = ((int)o[vp + 2] + o[prev_pos + 2]) / 2;
+            } else {
+                rr = o[prev_pos]; rg = o[prev_pos + 1]; rb = o[prev_pos + 2];
+            }
+            o[position] = (uint8_t)(rd - 3 + rr);
+            o[position + 1] = (uint8_t)(gd - 3 + rg);
+            o[position + 2] = (uint8_t)(bd - 3 + rb);
+            break;
+        }
+        case P_LUMA: {                                                   /* code.rs:619-629 */
+            unsigned k, gs, rs2, bs;
+            RS(S_LUMA_REF, k);
+            if (k >= 11) { rc = NICE_ORACLE_E_PANIC; goto done; }
+            size_t br = rel_ref[k];
+            RS(S_LUMA_BASE, gs);
+            uint8_t g = (uint8_t)(gs - 32);
+            size_t rp = position - br;
+            IDX(position + 2); IDX(rp + 2);
+            o[position + 1] = (uint8_t)(g + o[rp + 1]);
+            RS(S_LUMA_OTHER, rs2);
+            o[position] = (uint8_t)((uint8_t)(rs2 - 16) + (uint8_t)(g + o[rp]));
+            RS(S_LUMA_OTHER, bs);
+            o[position + 2] = (uint8_t)((uint8_t)(bs - 16) + (uint8_t)(g + o[rp + 2]));
+            break;
+        }
+        case P_BACK_REF: {                                               /* code.rs:630-637 */
+            unsigned k;
+            RS(S_BACK_REF, k);
+            if (k >= 5) { rc = NICE_ORACLE_E_PANIC; goto done; }
+            size_t rp = position - back_ref[k];
+            IDX(position + 2); IDX(rp + 2);
+            o[position] = o[rp]; o[position + 1] = o[rp + 1]; o[position + 2] = o[rp + 2];
+            break;
+        }
+        case P_RGB: {                                                    /* code.rs:638-644 */
+            size_t vp = position >= rowb ? position - rowb : prev_pos;
+            unsigned a0, a1, a2;
+            IDX(position + 2); IDX(prev_pos + 2); IDX(vp + 2);
+            RS(S_RGB, a0);
+            o[position] = (uint8_t)((int)(int16_t)a0 + ((int)o[vp] + o[prev_pos]) / 2);
+            RS(S_RGB, a1);
+            o[position + 1] = (uint8_t)((int)(int16_t)a1 + ((int)o[vp + 1] + o[prev_pos + 1]) / 2);
+            RS(S_RGB, a2);
+            o[position + 2] = (uint8_t)((int)(int16_t)a2 + ((int)o[vp + 2] + o[prev_pos + 2]) / 2);
+            break;
+        }
+        default:
+            break;                                                       /* eprintln!, continue */
+        }
+        prev_pos = position;
+        position += step;
+        RS(S_PREFIX, prefix);                                            /* code.rs:660 */
+        if (prefix >= P_RUN1 && prefix <= P_RUN1 + 7) {
+            uint8_t shift = 0;
+            size_t run = 0;
+            while (prefix >= P_RUN1 && prefix <= P_RUN1 + 7) {
+                run += (size_t)(prefix - 5) << (shift & 63u);
+                shift = (uint8_t)(shift + 3);
+                RS(S_PREFIX, prefix);
+            }
+            run += 1;
+            for (size_t i = 0; i < run; ++i) {                          /* code.rs:675-678 */
+                size_t dst = position + i * ch;
+                IDX(prev_pos + 2); IDX(dst + 2);
+                memmove(o + dst, o + prev_pos, 3);
+            }
+            position += run * ch;
+        }
+    }
+    (void)v;
+done:
+    for (int k = 0; k < N_STREAMS; ++k) free(L[k].lut);
+    if (rc) { free(o); return rc; }
+    *out = o;
+    *out_len = image_size;
+    return 0;
+#undef RS
+#undef IDX
+}
+
+void nice_oracle_free(void *p) { free(p); }
+
+/* ------------------------------------------------------------------------- */
+/* Known-answer helpers mirroring the reference's inline tests.               */
+/* ------------------------------------------------------------------------- */
+/* bitwriter.rs:86-97: write_8bits (2,3) x3 then (2,0). Returns bytes written. */
+int nice_oracle_kat_writer(uint8_t *out, int cap) {
+    sink_t s = {0};
+    bitwriter_t b = {&s, 0, 0};
+    bw_write_8bits(&b, 2, 3); bw_write_8bits(&b, 2, 3);
+    bw_write_8bits(&b, 2, 3); bw_write_8bits(&b, 2, 0);
+    int n = (int)s.len < cap ? (int)s.len : cap;
+    memcpy(out, s.p, (size_t)n);
+    free(s.p);
+    return n;
+}
+
+/* Sequence driver for the reader KATs (bitreader.rs:106-146).
+ * ops[i] = 0: read_bitsu8(bits[i]); 1: read_24bits(bits[i]); 2: read_24bits_noclear(bits[i]). */
+int nice_oracle_kat_reader(const uint8_t *data, size_t len, const int *ops, const int *bits,
+                           int n, uint32_t *results) {
+    bitreader_t r;
+    br_init(&r, data, len, 0);
+    for (int i = 0; i < n; ++i) {
+        if (ops[i] == 0) {
+            uint8_t v;
+            if (br_read_bitsu8(&r, (uint8_t)bits[i], &v)) return -1;
+            results[i] = v;
+        } else if (ops[i] == 1) {
+            results[i] = br_read_24bits(&r, (uint8_t)bits[i]);
+        } else {
+            results[i] = br_read_24bits_noclear(&r, (uint8_t)bits[i]);
+        }
+    }
+    return 0;
+}
+
+/* hfe.rs:300-348: one 256-symbol stream with counts i*10, encoded through
+ * to_encoded_output + appended cache, then decoded symbol by symbol.
+ * Returns 0 if every symbol round-trips; fills the stream length and max_aob. */
+int nice_oracle_kat_hfe(size_t *stream_len, uint8_t *max_aob) {
+    const int n = 256;
+    uint64_t *occ = (uint64_t *)calloc((size_t)n, 8);
+    for (int i = 0; i < n; ++i) occ[i] = (uint64_t)i * 10;
+    uint8_t *aob = (uint8_t *)malloc((size_t)n);
+    uint64_t *code = (uint64_t *)malloc(8 * (size_t)n);
+    nice_oracle_code_lengths(occ, n, aob);
+    nice_oracle_canonical(aob, n, code);
+    sink_t s = {0};
+    bitwriter_t b = {&s, 0, 0};
+    uint8_t mx = 0;
+    for (int i = 0; i < n; ++i) if (aob[i] > mx) mx = aob[i];
+    bw_write_8bits(&b, 5, mx);
+    uint8_t fb = field_bits(mx);
+    for (int i = 0; i < n; ++i) bw_write_8bits(&b, fb, aob[i]);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i * 10; ++j) bw_write_24bits(&b, aob[i], (uint32_t)code[i]);
+    sink_put(&s, (uint8_t)(b.cache >> 24));
+    for (int sh = 24; sh >= 0; sh -= 8) sink_put(&s, (uint8_t)(b.cache >> sh));
+    *stream_len = s.len;
+    *max_aob = mx;
+    bitreader_t r;
+    br_init(&r, s.p, s.len, 0);
+    sslookup_t sl = {0};
+    int rc = read_header_into_tree(&r, &sl, n);
+    for (int i = 0; i < n && !rc; ++i)
+        for (int j = 0; j < i * 10 && !rc; ++j) {
+            unsigned sym;
+            if (read_next_symbol(&r, &sl, &sym) || sym != (unsigned)i) rc = 1;
+        }
+    free(sl.lut); free(s.p); free(occ); free(aob); free(code);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic inputs.                                           */
+/* ------------------------------------------------------------------------- */
+void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed) {
+    static const int AMP[8] = {0, 1, 2, 3, 8, 24, 64, 256};
+    uint32_t s = seed;
+    for (uint32_t y = 0; y < H; ++y) {
+        int amp = AMP[(8ull * y) / H];
+        for (uint32_t x = 0; x < W; ++x) {
+            uint8_t *p = px + ((size_t)y * W + x) * C;
+            unsigned bx = W > 1 ? (200u * x) / (W - 1) : 0;
+            unsigned by = H > 1 ? (200u * y) / (H - 1) : 0;
+            unsigned base[3] = {bx, by, (bx + by) / 2};
+            if (((x / 16) + (y / 16)) % 7 == 0) {
+                p[0] = 40; p[1] = 80; p[2] = 120;
+            } else {
+                for (int c = 0; c < 3; ++c) {
+                    s ^= s << 13; s ^= s >> 17; s ^= s << 5;
+                    int n;
+                    if (amp == 0) n = 0;
+                    else if (amp < 256) n = (int)(s % (uint32_t)amp) - amp / 2;
+                    else n = (int)(s & 255u);
+                    p[c] = (uint8_t)((int)base[c] + n);
+                }
+            }
+            if (C == 4) p[3] = 255;
+        }
+    }
+}
+
+void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C) {
+    for (uint32_t y = 0; y < H; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            uint8_t *p = px + ((size_t)y * W + x) * C;
+            p[0] = (uint8_t)(W > 1 ? (255u * x) / (W - 1) : 0);
+            p[1] = (uint8_t)(H > 1 ? (255u * y) / (H - 1) : 0);
+            p[2] = (uint8_t)((W + H > 2) ? (255u * (x + y)) / (W + H - 2) : 0);
+            if (C == 4) p[3] = 255;
+        }
+}

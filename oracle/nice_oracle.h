@@ -1,0 +1,53 @@
+/* nice_oracle.h -- TEST INFRASTRUCTURE ONLY (see nice_oracle.c header).
+ * CPU restatement of the reference NICE2 encoder/decoder used as the parity
+ * checker and the timed CPU baseline.  Never linked into the product. */
+#ifndef NICE_ORACLE_H
+#define NICE_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    NICE_ORACLE_OK = 0,
+    NICE_ORACLE_E_ARG = -1,
+    NICE_ORACLE_E_OOM = -2,
+    NICE_ORACLE_E_PANIC = -3   /* the reference would panic (index OOB, EOF in read_exact, ...) */
+};
+
+enum { NICE_ORACLE_DEC_REFERENCE = 0, NICE_ORACLE_DEC_STRIDE = 1 };
+
+typedef struct {
+    uint8_t max_aob[10];       /* per-stream max code length (hfe.rs:97) */
+    uint8_t max_emitted_aob;   /* max code length over emitted symbols */
+    uint64_t n_symbols, n_coded, n_backref, n_smalldiff, n_luma2, n_luma, n_rgb, n_run_pixels;
+    uint64_t header_end;       /* file bytes written before the first data symbol */
+    uint64_t hist_total;
+    uint64_t hist[858];        /* symbol counts, streams concatenated in id order */
+    uint8_t aob[858];          /* code lengths, same layout */
+} nice_oracle_stats;
+
+int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+                       uint8_t channels, uint8_t channels_out,
+                       uint8_t **out, size_t *out_len, nice_oracle_stats *stats);
+int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, size_t *out_len,
+                       uint32_t *w, uint32_t *h, uint8_t *ch);
+void nice_oracle_free(void *p);
+
+void nice_oracle_code_lengths(const uint64_t *counts, int n, uint8_t *aob);
+void nice_oracle_canonical(const uint8_t *aob, int n, uint64_t *code);
+
+int nice_oracle_kat_writer(uint8_t *out, int cap);
+int nice_oracle_kat_reader(const uint8_t *data, size_t len, const int *ops, const int *bits,
+                           int n, uint32_t *results);
+int nice_oracle_kat_hfe(size_t *stream_len, uint8_t *max_aob);
+
+void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed);
+void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
