@@ -1,0 +1,228 @@
+"""MI355X-native NICE2 codec: host-side mirror of the reference codec API.
+
+The reference (Rust, wouter-rombouts/fast-losless-image-compression-format)
+exposes its codec path as
+
+* ``image::Image::new(width, height, channels)``          image.rs:22-43
+* ``code::encode(input_bytes, image_header, channels_out, output_writer)``
+                                                            code.rs:59-64
+* ``code::decode(image_reader, channels_out, output_vec) -> Image``
+                                                            code.rs:464-468
+
+This package keeps those names and argument meanings and forwards to the C ABI
+in ``libnice_hip.so`` (include/nice.h), whose kernels run on the GPU.  There is
+no CPU fallback: if the library or a gfx950 device is missing, every call raises.
+
+Device-resident batches (the benchmark path) go through ``encode_batch`` and
+``decode_batch`` which take torch tensors already on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import io
+import os
+from dataclasses import dataclass
+
+__all__ = [
+    "Image", "encode", "decode", "encode_bytes", "decode_bytes", "encode_bound",
+    "encode_batch", "decode_batch", "NiceError", "lib", "LIB_PATH",
+    "DEC_STRICT_REFERENCE", "DEC_ALPHA_FILL_FF",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnice_hip.so")
+
+OK, E_ARG, E_HIP, E_NODEV, E_CAPACITY, E_FORMAT, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+_ERRNAMES = {E_ARG: "bad argument", E_HIP: "HIP runtime failure", E_NODEV: "no gfx950 device",
+             E_CAPACITY: "output buffer too small",
+             E_FORMAT: "malformed stream (the reference decoder would panic)",
+             E_UNSUPPORTED: "stream outside the reference decoder's domain"}
+DEC_STRICT_REFERENCE = 0x1
+DEC_ALPHA_FILL_FF = 0x2
+
+EXPORTS = [
+    "nice_version", "nice_device_count", "nice_encode_bound", "nice_encode", "nice_peek_header",
+    "nice_decode", "nice_ctx_create", "nice_ctx_destroy", "nice_ctx_reserve",
+    "nice_encode_batch_dev", "nice_decode_batch_dev",
+]
+
+
+class NiceError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {_ERRNAMES.get(code, 'error')} ({code})")
+
+
+_lib = None
+
+
+def lib():
+    """Load libnice_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NiceError(E_NODEV, f"{LIB_PATH} missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    u32 = ctypes.c_uint32
+    u64 = ctypes.c_uint64
+    L.nice_version.restype = ctypes.c_char_p
+    L.nice_encode_bound.restype = sz
+    L.nice_encode_bound.argtypes = [u32, u32]
+    L.nice_encode.argtypes = [u8p, sz, u32, u32, ctypes.c_uint8, ctypes.c_uint8, u8p, sz,
+                              ctypes.POINTER(sz)]
+    L.nice_peek_header.argtypes = [u8p, sz, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                   ctypes.POINTER(ctypes.c_uint8)]
+    L.nice_decode.argtypes = [u8p, sz, u8p, sz, u32, ctypes.POINTER(sz)]
+    L.nice_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.nice_ctx_destroy.argtypes = [ctypes.c_void_p]
+    L.nice_ctx_reserve.argtypes = [ctypes.c_void_p, u32, u32, u32]
+    L.nice_encode_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u64, u32, u32, u32,
+                                        ctypes.c_uint8, ctypes.c_uint8, u8p, u64, u8p]
+    L.nice_decode_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u64, u8p, u32, u32,
+                                        u32, ctypes.c_uint8, u8p, u64, u32, u8p]
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != OK:
+        raise NiceError(rc, what)
+
+
+@dataclass
+class Image:
+    """image.rs:5-43 -- only width/height/channels are used on the codec path."""
+    width: int
+    height: int
+    channels: int
+
+    @staticmethod
+    def new(width: int, height: int, channels: int) -> "Image":
+        return Image(width, height, channels)
+
+
+def encode_bound(width: int, height: int) -> int:
+    return int(lib().nice_encode_bound(width, height))
+
+
+def _as_buffer(data):
+    """(ctypes pointer, nbytes, keepalive) for bytes / bytearray / numpy / memoryview."""
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        buf = (ctypes.c_uint8 * mv.nbytes).from_buffer_copy(mv)
+    else:
+        buf = (ctypes.c_uint8 * mv.nbytes).from_buffer(mv)
+    return ctypes.cast(buf, ctypes.c_void_p), mv.nbytes, buf
+
+
+def encode_bytes(input_bytes, width: int, height: int, channels: int,
+                 channels_out: int | None = None) -> bytes:
+    ptr, n, keep = _as_buffer(input_bytes)
+    cap = encode_bound(width, height)
+    out = (ctypes.c_uint8 * cap)()
+    out_len = ctypes.c_size_t()
+    co = channels if channels_out is None else channels_out
+    rc = lib().nice_encode(ptr, n, width, height, channels, co, out, cap, ctypes.byref(out_len))
+    _check(rc, "nice_encode")
+    del keep
+    return bytes(out[: out_len.value])
+
+
+def encode(input_bytes, image_header: Image, channels_out: int, output_writer) -> None:
+    """code::encode (code.rs:59-64): appends the stream to ``output_writer``
+    (a bytearray, or any object with ``write``)."""
+    data = encode_bytes(input_bytes, image_header.width, image_header.height,
+                        image_header.channels, channels_out)
+    if isinstance(output_writer, bytearray):
+        output_writer.extend(data)
+    else:
+        output_writer.write(data)
+
+
+def decode_bytes(stream, flags: int = DEC_ALPHA_FILL_FF):
+    """Returns (pixels: bytes, Image)."""
+    ptr, n, keep = _as_buffer(stream)
+    w, h, ch = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint8()
+    _check(lib().nice_peek_header(ptr, n, ctypes.byref(w), ctypes.byref(h), ctypes.byref(ch)),
+           "nice_peek_header")
+    cap = w.value * h.value * max(ch.value, 1)
+    out = (ctypes.c_uint8 * max(cap, 1))()
+    px_len = ctypes.c_size_t()
+    rc = lib().nice_decode(ptr, n, out, cap, flags, ctypes.byref(px_len))
+    _check(rc, "nice_decode")
+    del keep
+    return bytes(out[: px_len.value]), Image(w.value, h.value, ch.value)
+
+
+def decode(image_reader, channels_out: int, output_vec: bytearray) -> Image:
+    """code::decode (code.rs:464-468).  ``channels_out`` is accepted and ignored,
+    as in the reference (main.rs:88 passes 3; code.rs never reads it).  The
+    output replaces ``output_vec``'s contents."""
+    del channels_out
+    data = image_reader.read() if hasattr(image_reader, "read") else bytes(image_reader)
+    px, img = decode_bytes(data)
+    output_vec[:] = px
+    return img
+
+
+# ---- device-resident batches (torch tensors on the GPU) ---------------------
+class _Ctx:
+    def __init__(self, device: int):
+        self.ptr = ctypes.c_void_p()
+        _check(lib().nice_ctx_create(device, ctypes.byref(self.ptr)), "nice_ctx_create")
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().nice_ctx_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+_ctxs: dict = {}
+
+
+def _ctx(device: int) -> _Ctx:
+    if device not in _ctxs:
+        _ctxs[device] = _Ctx(device)
+    return _ctxs[device]
+
+
+def _stream_ptr(torch, device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def encode_batch(px, width: int, height: int, channels: int, out, out_len,
+                 channels_out: int | None = None, stream=None) -> None:
+    """Encode ``px`` (uint8 cuda tensor [n_frames, W*H*channels]) into ``out``
+    (uint8 cuda tensor [n_frames, stride >= encode_bound]); lengths into
+    ``out_len`` (int64 cuda tensor [n_frames]).  Asynchronous on the current
+    torch stream (or ``stream``: a torch.cuda.Stream)."""
+    import torch
+    dev = px.device.index or 0
+    n = px.shape[0]
+    st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(torch, px.device)
+    rc = lib().nice_encode_batch_dev(
+        _ctx(dev).ptr, st, ctypes.c_void_p(px.data_ptr()), px.stride(0), n, width, height,
+        channels, channels if channels_out is None else channels_out,
+        ctypes.c_void_p(out.data_ptr()), out.stride(0), ctypes.c_void_p(out_len.data_ptr()))
+    _check(rc, "nice_encode_batch_dev")
+
+
+def decode_batch(streams, stream_len, width: int, height: int, out_channels: int, px, status,
+                 flags: int = DEC_ALPHA_FILL_FF, stream=None) -> None:
+    """Decode ``streams`` (uint8 cuda [n, stride]) with byte lengths ``stream_len``
+    (int64 cuda [n]) into ``px`` (uint8 cuda [n, >= W*H*out_channels]); per-frame
+    status codes into ``status`` (int32 cuda [n])."""
+    import torch
+    dev = streams.device.index or 0
+    n = streams.shape[0]
+    st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(torch, streams.device)
+    rc = lib().nice_decode_batch_dev(
+        _ctx(dev).ptr, st, ctypes.c_void_p(streams.data_ptr()), streams.stride(0),
+        ctypes.c_void_p(stream_len.data_ptr()), n, width, height, out_channels,
+        ctypes.c_void_p(px.data_ptr()), px.stride(0), flags, ctypes.c_void_p(status.data_ptr()))
+    _check(rc, "nice_decode_batch_dev")

@@ -1,0 +1,450 @@
+// nice_capi.hip -- host runtime behind include/nice.h: contexts, scratch arenas,
+// kernel launch sequences and the host-buffer convenience entry points.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/nice.h"
+#include "nice_format.h"
+#include "nice_bits.hpp"
+#include "nice_kernels.h"
+
+using namespace nice;
+
+#define NICE_HIP(x)                          \
+  do {                                       \
+    if ((x) != hipSuccess) return NICE_E_HIP; \
+  } while (0)
+
+namespace {
+
+// Device scratch arena, grown on demand (reserve() to pre-size).
+struct Arena {
+  void* ptr = nullptr;
+  size_t cap = 0;
+  int grow(size_t bytes) {
+    if (bytes <= cap) return NICE_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    if (hipMalloc(&ptr, bytes) != hipSuccess) return NICE_E_HIP;
+    cap = bytes;
+    return NICE_OK;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+  }
+};
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Encoder scratch layout. The zero-per-launch block comes first (memset once).
+struct EncLayout {
+  size_t zero_bytes, total;
+  size_t o_hist, o_flags, o_ticket, o_desc;
+  size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
+      o_hdrbytes, o_hdrcache, o_hdrbitoff;
+};
+
+EncLayout enc_layout(uint32_t n_frames, uint32_t T) {
+  EncLayout L{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
+  L.o_hist = take((size_t)n_frames * N_BINS * 4);
+  L.o_flags = take((size_t)n_frames * 4);
+  L.o_ticket = take(16);
+  L.o_desc = take((size_t)n_frames * T * 16);
+  L.zero_bytes = align_up(o, 16);
+  L.o_first = take((size_t)n_frames * T * 4);
+  L.o_last = take((size_t)n_frames * T * 4);
+  L.o_next = take((size_t)n_frames * T * 4);
+  L.o_tbl = take((size_t)n_frames * N_BINS * 4);
+  L.o_tblcode = take((size_t)n_frames * N_BINS * 4);
+  L.o_len8 = take((size_t)n_frames * N_BINS);
+  L.o_smax = take((size_t)n_frames * N_STREAMS);
+  L.o_seedbit = take((size_t)n_frames * 8);
+  L.o_seedsuf = take((size_t)n_frames * 4);
+  L.o_hdrbytes = take((size_t)n_frames * 8);
+  L.o_hdrcache = take((size_t)n_frames * 4);
+  L.o_hdrbitoff = take((size_t)n_frames);
+  L.total = o;
+  return L;
+}
+
+int g_device_ok = -1;
+
+int check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return NICE_E_NODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return NICE_E_NODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NICE_E_NODEV;
+  return NICE_OK;
+}
+
+}  // namespace
+
+struct nice_ctx {
+  int device = 0;
+  std::mutex mu;
+  Arena enc, dec, host_px, host_out, dev_len;
+};
+
+extern "C" {
+
+const char* nice_version(void) { return "nice-mi355x 0.1 (gfx950)"; }
+
+int nice_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+size_t nice_encode_bound(uint32_t w, uint32_t h) {
+  // Huffman cost <= fixed-length cost per stream: <= 28 bits per coded pixel,
+  // <= 2 bits per run pixel for digits (code.rs:391-406). Table header <= 858
+  // 8-bit fields + 10 5-bit fields. 32 bits/px keeps it simple and word aligned.
+  return (size_t)FILE_HEADER_BYTES + 880 + (size_t)w * h * 4 + 32;
+}
+
+int nice_peek_header(const uint8_t* s, size_t len, uint32_t* w, uint32_t* h, uint8_t* ch) {
+  if (!s || len < 13) return NICE_E_FORMAT;
+  if (w) *w = ((uint32_t)s[4] << 24) | ((uint32_t)s[5] << 16) | ((uint32_t)s[6] << 8) | s[7];
+  if (h) *h = ((uint32_t)s[8] << 24) | ((uint32_t)s[9] << 16) | ((uint32_t)s[10] << 8) | s[11];
+  if (ch) *ch = s[12];
+  return NICE_OK;
+}
+
+int nice_ctx_create(int device, nice_ctx** out) {
+  if (!out) return NICE_E_ARG;
+  int rc = check_device(device);
+  if (rc) return rc;
+  nice_ctx* c = new nice_ctx();
+  c->device = device;
+  *out = c;
+  return NICE_OK;
+}
+
+void nice_ctx_destroy(nice_ctx* ctx) {
+  if (!ctx) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(ctx->device);
+  ctx->enc.release();
+  ctx->dec.release();
+  ctx->host_px.release();
+  ctx->host_out.release();
+  ctx->dev_len.release();
+  (void)hipSetDevice(prev);
+  delete ctx;
+}
+
+static uint32_t tiles_for(uint32_t w, uint32_t h) {
+  const uint64_t N = (uint64_t)w * h;
+  return (uint32_t)((N + ENC_TILE - 1) / ENC_TILE);
+}
+
+int nice_ctx_reserve(nice_ctx* ctx, uint32_t n_frames, uint32_t w, uint32_t h) {
+  if (!ctx) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  EncLayout L = enc_layout(n_frames, tiles_for(w, h));
+  return ctx->enc.grow(L.total);
+}
+
+int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t frame_stride,
+                          uint32_t n_frames, uint32_t w, uint32_t h, uint8_t channels,
+                          uint8_t channels_out, uint8_t* d_out, uint64_t out_stride,
+                          uint64_t* d_out_len) {
+  if (!ctx || !d_out || !d_out_len) return NICE_E_ARG;
+  if (channels != 3 && channels != 4) return NICE_E_ARG;
+  const uint64_t N = (uint64_t)w * h;
+  if (N > (1ull << 30)) return NICE_E_ARG;
+  if (n_frames == 0) return NICE_OK;
+  if (N > 0 && !d_px) return NICE_E_ARG;
+  if (out_stride < nice_encode_bound(w, h) || (out_stride & 3) || ((uintptr_t)d_out & 3))
+    return NICE_E_ARG;
+  if (channels == 4 && N > 0 && (((uintptr_t)d_px & 3) || (frame_stride & 3))) return NICE_E_ARG;
+  if (N > 0 && frame_stride < N * channels) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t T = tiles_for(w, h);
+  EncLayout L = enc_layout(n_frames, T);
+  int rc = ctx->enc.grow(L.total);
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)ctx->enc.ptr;
+  EncArgs a{};
+  a.px = d_px;
+  a.frame_stride = frame_stride;
+  a.n_frames = n_frames;
+  a.W = w;
+  a.H = h;
+  a.C = channels;
+  a.channels_out = channels_out;
+  a.tiles_per_frame = T;
+  a.out = d_out;
+  a.out_stride = out_stride;
+  a.out_len = (unsigned long long*)d_out_len;
+  a.hist = (uint32_t*)(base + L.o_hist);
+  a.frame_flags = (uint32_t*)(base + L.o_flags);
+  a.ticket = (uint32_t*)(base + L.o_ticket);
+  a.tiles_desc = base + L.o_desc;
+  a.tile_first = (uint32_t*)(base + L.o_first);
+  a.tile_last = (uint32_t*)(base + L.o_last);
+  a.tile_next = (uint32_t*)(base + L.o_next);
+  a.tbl = (uint32_t*)(base + L.o_tbl);
+  a.tbl_code = (uint32_t*)(base + L.o_tblcode);
+  a.tbl_len8 = base + L.o_len8;
+  a.stream_max = base + L.o_smax;
+  a.seed_bit = (unsigned long long*)(base + L.o_seedbit);
+  a.seed_suf = (uint32_t*)(base + L.o_seedsuf);
+  a.hdr_bytes = (unsigned long long*)(base + L.o_hdrbytes);
+  a.hdr_cache = (uint32_t*)(base + L.o_hdrcache);
+  a.hdr_bitoff = base + L.o_hdrbitoff;
+
+  NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
+  const uint64_t total_tiles = (uint64_t)n_frames * T;
+  if (T > 0) {
+    // contiguous tile chunks per block: keeps rows-above reuse in L2 and
+    // flushes each block's LDS histogram once per frame
+    uint64_t blocks = 2048;
+    uint64_t per = (total_tiles + blocks - 1) / blocks;
+    if (per < 1) per = 1;
+    blocks = (total_tiles + per - 1) / per;
+    a.tiles_per_block = (uint32_t)per;
+    hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_tailruns, dim3(n_frames), dim3(1024), 0, st, a);
+  }
+  hipLaunchKernelGGL(enc_tables, dim3(n_frames * N_STREAMS), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(enc_header, dim3(n_frames), dim3(64), 0, st, a);
+  if (T > 0) {
+    hipLaunchKernelGGL(enc_pack, dim3((uint32_t)total_tiles), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_serial, dim3(n_frames), dim3(64), 0, st, a);
+  }
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+
+// ---- decoder ---------------------------------------------------------------
+namespace {
+struct DecLayout {
+  size_t total;
+  size_t o_tables, o_dstart, o_ea, o_eb, o_cpx, o_cstart, o_bounds, o_changed, o_rowbuf;
+};
+DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t H, uint32_t nseg, size_t rowbuf) {
+  DecLayout L{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
+  L.o_tables = take((size_t)n_frames * sizeof(DecTables));
+  L.o_dstart = take((size_t)n_frames * 8);
+  L.o_ea = take((size_t)n_frames * max_chunks * sizeof(ParseState));
+  L.o_eb = take((size_t)n_frames * max_chunks * sizeof(ParseState));
+  L.o_cpx = take((size_t)n_frames * max_chunks * 8);
+  L.o_cstart = take((size_t)n_frames * max_chunks * 8);
+  L.o_bounds = take((size_t)n_frames * H * nseg * sizeof(SegBound));
+  L.o_changed = take(16);
+  L.o_rowbuf = take(rowbuf);
+  L.total = o;
+  return L;
+}
+struct RecGeom {
+  uint32_t seg, nseg, R;
+  size_t lds;
+  bool in_lds;
+};
+RecGeom rec_geom(uint32_t w) {
+  RecGeom g;
+  uint32_t s = (w + DEC_MAX_SEGS - 1) / DEC_MAX_SEGS;
+  if (s < 6) s = 6;
+  g.seg = s;
+  g.nseg = w ? (w + s - 1) / s : 1;
+  g.R = w >= 3 ? 4 : 8;
+  const size_t kw = (w + 31) / 32;
+  const size_t head = align_up((sizeof(DecTables) + 7 * 4), 16) + align_up(kw, 4) * 4;
+  const size_t ring = (size_t)g.R * w * 4;
+  g.in_lds = head + ring <= 150 * 1024;
+  g.lds = g.in_lds ? head + ring : head;
+  return g;
+}
+}  // namespace
+
+// ---- context-free host-buffer entry points --------------------------------
+static std::mutex g_default_mu;
+static nice_ctx* g_default = nullptr;
+
+static int default_ctx(nice_ctx** out) {
+  std::lock_guard<std::mutex> g(g_default_mu);
+  if (!g_default) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int rc = nice_ctx_create(dev, &g_default);
+    if (rc) return rc;
+  }
+  *out = g_default;
+  return NICE_OK;
+}
+
+int nice_encode(const uint8_t* px, size_t px_len, uint32_t w, uint32_t h, uint8_t channels,
+                uint8_t channels_out, uint8_t* out, size_t out_cap, size_t* out_len) {
+  if (!out || !out_len) return NICE_E_ARG;
+  if (channels != 3 && channels != 4) return NICE_E_ARG;
+  const uint64_t N = (uint64_t)w * h;
+  if (px_len < N * channels || (N > 0 && !px)) return NICE_E_ARG;
+  nice_ctx* ctx;
+  int rc = default_ctx(&ctx);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  NICE_HIP(hipSetDevice(ctx->device));
+  const size_t in_bytes = align_up((size_t)N * channels, 256);
+  const size_t bound = align_up(nice_encode_bound(w, h), 256);
+  if ((rc = ctx->host_px.grow(in_bytes + 256))) return rc;
+  if ((rc = ctx->host_out.grow(bound))) return rc;
+  if ((rc = ctx->dev_len.grow(256))) return rc;
+  if (N) NICE_HIP(hipMemcpy(ctx->host_px.ptr, px, (size_t)N * channels, hipMemcpyHostToDevice));
+  rc = nice_encode_batch_dev(ctx, nullptr, (const uint8_t*)ctx->host_px.ptr, in_bytes, 1, w, h,
+                             channels, channels_out, (uint8_t*)ctx->host_out.ptr, bound,
+                             (uint64_t*)ctx->dev_len.ptr);
+  if (rc) return rc;
+  uint64_t n = 0;
+  NICE_HIP(hipMemcpy(&n, ctx->dev_len.ptr, 8, hipMemcpyDeviceToHost));
+  if (n > out_cap) {
+    *out_len = n;
+    return NICE_E_CAPACITY;
+  }
+  NICE_HIP(hipMemcpy(out, ctx->host_out.ptr, n, hipMemcpyDeviceToHost));
+  *out_len = n;
+  return NICE_OK;
+}
+
+
+int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
+                          uint64_t stream_stride, const uint64_t* d_stream_len, uint32_t n_frames,
+                          uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
+                          uint64_t px_stride, uint32_t flags, int32_t* d_status) {
+  if (!ctx || !d_streams || !d_stream_len || !d_status) return NICE_E_ARG;
+  if (out_channels != 3 && out_channels != 4) return NICE_E_ARG;
+  if ((stream_stride & 3) || ((uintptr_t)d_streams & 3)) return NICE_E_ARG;
+  const uint64_t N = (uint64_t)w * h;
+  if (N > (1ull << 30)) return NICE_E_ARG;
+  if (n_frames == 0) return NICE_OK;
+  if (N > 0 && (!d_px || px_stride < N * out_channels)) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  NICE_HIP(hipMemsetAsync(d_status, 0, (size_t)n_frames * 4, st));
+  // stream lengths bound the chunk grid
+  std::vector<uint64_t> lens(n_frames);
+  NICE_HIP(hipMemcpyAsync(lens.data(), d_stream_len, (size_t)n_frames * 8, hipMemcpyDeviceToHost, st));
+  NICE_HIP(hipStreamSynchronize(st));
+  uint64_t max_len = 0;
+  for (uint64_t l : lens) {
+    if (l > stream_stride) return NICE_E_ARG;
+    max_len = l > max_len ? l : max_len;
+  }
+  const uint64_t D = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
+  const uint32_t max_chunks =
+      max_len * 8 > D ? (uint32_t)((max_len * 8 - D + DEC_CHUNK_BITS - 1) / DEC_CHUNK_BITS) : 1;
+  const RecGeom g = rec_geom(w);
+  const size_t rowbuf = g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4;
+  DecLayout L = dec_layout(n_frames, max_chunks, h, g.nseg, rowbuf);
+  int rc = ctx->dec.grow(L.total);
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)ctx->dec.ptr;
+  DecArgs a{};
+  a.streams = d_streams;
+  a.stream_stride = stream_stride;
+  a.stream_len = (const unsigned long long*)d_stream_len;
+  a.n_frames = n_frames;
+  a.W = w;
+  a.H = h;
+  a.out_channels = out_channels;
+  a.flags = flags;
+  a.px_out = d_px;
+  a.px_stride = px_stride;
+  a.status = d_status;
+  a.tables = base + L.o_tables;
+  a.data_start = (unsigned long long*)(base + L.o_dstart);
+  a.max_chunks = max_chunks;
+  a.chunk_blocks = (max_chunks + 255) / 256;
+  a.chunk_px = (unsigned long long*)(base + L.o_cpx);
+  a.chunk_start = (unsigned long long*)(base + L.o_cstart);
+  a.bounds = base + L.o_bounds;
+  a.seg = g.seg;
+  a.nseg = g.nseg;
+  a.rows_in_lds = g.in_lds ? 1u : 0u;
+  a.rowbuf = (uint32_t*)(base + L.o_rowbuf);
+  ParseState* ea = (ParseState*)(base + L.o_ea);
+  ParseState* eb = (ParseState*)(base + L.o_eb);
+  uint32_t* changed = (uint32_t*)(base + L.o_changed);
+
+  hipLaunchKernelGGL(dec_tables, dim3(n_frames), dim3(256), 0, st, a);
+  if (N == 0) {
+    NICE_HIP(hipGetLastError());
+    return NICE_OK;
+  }
+  hipLaunchKernelGGL(dec_init_entries, dim3((max_chunks + 255) / 256 < 64 ? (max_chunks + 255) / 256 : 64, n_frames),
+                     dim3(256), 0, st, a, ea);
+  const dim3 cgrid(n_frames * a.chunk_blocks);
+  // Jacobi iteration of the chunk entry states to the fixpoint
+  uint32_t host_changed = 1;
+  for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it) {
+    NICE_HIP(hipMemsetAsync(changed, 0, 4, st));
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, (const ParseState*)ea, eb, changed);
+    NICE_HIP(hipMemcpyAsync(&host_changed, changed, 4, hipMemcpyDeviceToHost, st));
+    NICE_HIP(hipStreamSynchronize(st));
+    ParseState* t = ea;
+    ea = eb;
+    eb = t;
+  }
+  hipLaunchKernelGGL(dec_count, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(dec_bounds, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  if (g.lds > 64 * 1024)
+    NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+  hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+int nice_decode(const uint8_t* s, size_t len, uint8_t* px_out, size_t cap, uint32_t flags,
+                size_t* px_len) {
+  uint32_t w, h;
+  uint8_t ch;
+  int rc = nice_peek_header(s, len, &w, &h, &ch);
+  if (rc) return rc;
+  if (ch != 3 && ch != 4) return NICE_E_UNSUPPORTED;
+  if ((flags & NICE_DEC_STRICT_REFERENCE) && ch != 3) return NICE_E_UNSUPPORTED;
+  const uint64_t N = (uint64_t)w * h;
+  if (N > (1ull << 30)) return NICE_E_ARG;
+  if (px_len) *px_len = (size_t)N * ch;
+  if (cap < N * ch || (N && !px_out)) return NICE_E_CAPACITY;
+  nice_ctx* ctx;
+  if ((rc = default_ctx(&ctx))) return rc;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  NICE_HIP(hipSetDevice(ctx->device));
+  const size_t sbytes = align_up(len + 8, 256);
+  const size_t pbytes = align_up((size_t)N * ch + 4, 256);
+  if ((rc = ctx->host_out.grow(sbytes))) return rc;
+  if ((rc = ctx->host_px.grow(pbytes))) return rc;
+  if ((rc = ctx->dev_len.grow(256))) return rc;
+  NICE_HIP(hipMemcpy(ctx->host_out.ptr, s, len, hipMemcpyHostToDevice));
+  uint64_t l64 = len;
+  NICE_HIP(hipMemcpy(ctx->dev_len.ptr, &l64, 8, hipMemcpyHostToDevice));
+  int32_t* d_status = (int32_t*)((uint8_t*)ctx->dev_len.ptr + 64);
+  rc = nice_decode_batch_dev(ctx, nullptr, (const uint8_t*)ctx->host_out.ptr, sbytes,
+                             (const uint64_t*)ctx->dev_len.ptr, 1, w, h, ch,
+                             (uint8_t*)ctx->host_px.ptr, pbytes, flags, d_status);
+  if (rc) return rc;
+  int32_t status = 0;
+  NICE_HIP(hipMemcpy(&status, d_status, 4, hipMemcpyDeviceToHost));
+  if (status) return status;
+  if (N) NICE_HIP(hipMemcpy(px_out, ctx->host_px.ptr, (size_t)N * ch, hipMemcpyDeviceToHost));
+  return NICE_OK;
+}
+
+}  // extern "C"

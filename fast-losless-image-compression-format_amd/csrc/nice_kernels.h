@@ -1,0 +1,91 @@
+// nice_kernels.h -- kernel argument blocks and launch-visible constants shared by
+// the HIP kernels and the host runtime (nice_capi.hip).  Device pointers only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nice {
+
+constexpr int ENC_TILE = 1024;          // pixels per encoder tile (raster-contiguous)
+constexpr uint32_t FLAG_SERIAL = 1u;    // frame needs the exact serial writer
+
+struct EncArgs {
+  // input: n_frames frames of W*H pixels, C bytes per pixel, frame_stride bytes apart
+  const uint8_t* px;
+  uint64_t frame_stride;
+  uint32_t n_frames, W, H, C;
+  uint8_t channels_out;
+  uint32_t tiles_per_frame, tiles_per_block;
+  // output: frame f at out + f*out_stride, byte length in out_len[f]
+  uint8_t* out;
+  uint64_t out_stride;
+  unsigned long long* out_len;
+  // scratch (see nice_capi.hip for sizes)
+  uint32_t* hist;            // n_frames * 858
+  uint32_t* tile_first;      // n_frames * T
+  uint32_t* tile_last;       // n_frames * T
+  uint32_t* tile_next;       // n_frames * T
+  uint32_t* tbl;             // n_frames * 858: (code << 5) | len for len <= 25
+  uint32_t* tbl_code;        // n_frames * 858: code as u32 (serial path)
+  uint8_t* tbl_len8;         // n_frames * 858: u8 length
+  uint8_t* stream_max;       // n_frames * 10
+  uint32_t* frame_flags;     // n_frames
+  unsigned long long* seed_bit;   // n_frames: absolute bit where symbol data starts
+  uint32_t* seed_suf;        // n_frames: last 32 bits before seed_bit
+  unsigned long long* hdr_bytes;  // n_frames (serial header path)
+  uint32_t* hdr_cache;       // n_frames
+  uint8_t* hdr_bitoff;       // n_frames
+  void* tiles_desc;          // n_frames * T * 16 bytes, zeroed per launch
+  uint32_t* ticket;          // zeroed per launch
+};
+
+__global__ void enc_classify(EncArgs a);
+__global__ void enc_tailruns(EncArgs a);
+__global__ void enc_tables(EncArgs a);
+__global__ void enc_header(EncArgs a);
+__global__ void enc_pack(EncArgs a);
+__global__ void enc_serial(EncArgs a);
+
+}  // namespace nice
+
+namespace nice {
+
+constexpr uint32_t DEC_CHUNK_BITS = 2048;   // speculative-parse slice
+constexpr int DEC_MAX_SEGS = 64;            // one lane per row segment
+
+struct SegBound {
+  unsigned long long pos;   // bit position of the next coded pixel's prefix
+  unsigned long long run;   // run pixels (copies of the left neighbour) before it
+};
+
+struct DecArgs {
+  const uint8_t* streams;
+  uint64_t stream_stride;
+  const unsigned long long* stream_len;
+  uint32_t n_frames, W, H;
+  uint32_t out_channels, flags;
+  uint8_t* px_out;
+  uint64_t px_stride;
+  int32_t* status;
+  // scratch
+  void* tables;                       // n_frames DecTables
+  unsigned long long* data_start;     // n_frames
+  uint32_t max_chunks, chunk_blocks;  // per frame
+  unsigned long long* chunk_px;       // n_frames * max_chunks
+  unsigned long long* chunk_start;    // n_frames * max_chunks
+  void* bounds;                       // n_frames * H * nseg SegBound
+  uint32_t seg, nseg;
+  uint32_t rows_in_lds;               // 1: row ring in LDS, 0: in rowbuf
+  uint32_t* rowbuf;                   // n_frames * R * W (when not in LDS)
+};
+
+struct ParseState;
+__global__ void dec_tables(DecArgs a);
+__global__ void dec_init_entries(DecArgs a, ParseState* e);
+__global__ void dec_sync(DecArgs a, const ParseState* in, ParseState* out, uint32_t* changed);
+__global__ void dec_count(DecArgs a, const ParseState* entry);
+__global__ void dec_scan(DecArgs a);
+__global__ void dec_bounds(DecArgs a, const ParseState* entry);
+__global__ void dec_reconstruct(DecArgs a);
+
+}  // namespace nice

@@ -1,0 +1,94 @@
+/* nice.h -- C ABI of the MI355X-native NICE2 codec (libnice_hip.so).
+ *
+ * Drop-in boundary for the reference's codec entry points:
+ *   code::encode  /root/reference/src/code.rs:59-64
+ *       pub fn encode<W: io::Write>(input_bytes: &[u8], image_header: Image,
+ *                                   channels_out: u8, output_writer: &mut W)
+ *   code::decode  /root/reference/src/code.rs:464-468
+ *       pub fn decode<R: io::Read>(image_reader: &mut R, channels_out: u8,
+ *                                  output_vec: &mut Vec<u8>) -> io::Result<Image>
+ *   image::Image::new  /root/reference/src/image.rs:22-43 (width, height, channels)
+ *
+ * Plain pointers and sizes only.  Every function returns a status code (0 = ok,
+ * negative = error) and never aborts, where the reference panics/aborts
+ * (Cargo.toml:16 panic = "abort").  Buffers are caller-owned.  Functions taking a
+ * nice_ctx are thread-safe per context; the context-free functions use an
+ * internal per-device context guarded by a mutex.
+ */
+#ifndef NICE_H
+#define NICE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  NICE_OK = 0,
+  NICE_E_ARG = -1,          /* bad argument (sizes, channels, alignment) */
+  NICE_E_HIP = -2,          /* HIP runtime failure */
+  NICE_E_NODEV = -3,        /* no usable gfx950 device */
+  NICE_E_CAPACITY = -4,     /* output buffer too small */
+  NICE_E_FORMAT = -5,       /* malformed stream: the reference would panic here */
+  NICE_E_UNSUPPORTED = -6   /* stream outside the reference decoder's domain (see flags) */
+};
+
+/* nice_decode flags */
+#define NICE_DEC_STRICT_REFERENCE 0x1u /* fail wherever the reference decoder would fail */
+#define NICE_DEC_ALPHA_FILL_FF 0x2u    /* 4-channel output: write A = 255 */
+
+typedef struct nice_ctx nice_ctx;
+
+/* Library / device queries. */
+const char* nice_version(void);
+int nice_device_count(void);
+
+/* Upper bound of an encoded stream for a w x h image (any channels). */
+size_t nice_encode_bound(uint32_t w, uint32_t h);
+
+/* Replaces code::encode (code.rs:59-64): host pixels in, host stream out.
+ * px: w*h pixels of `channels` (3 or 4) bytes; only bytes +0..+2 of each pixel
+ * are coded (code.rs:197,215-217).  channels_out is written to header byte 12
+ * (code.rs:84).  *out_len receives the stream length. */
+int nice_encode(const uint8_t* px, size_t px_len, uint32_t w, uint32_t h, uint8_t channels,
+                uint8_t channels_out, uint8_t* out, size_t out_cap, size_t* out_len);
+
+/* Parses the 13-byte file header (code.rs:469-483). */
+int nice_peek_header(const uint8_t* s, size_t len, uint32_t* w, uint32_t* h, uint8_t* ch);
+
+/* Replaces code::decode (code.rs:464-468): host stream in, host pixels out.
+ * Output pixel stride = header channels byte (3: RGB; 4: RGB + alpha byte, 255
+ * with NICE_DEC_ALPHA_FILL_FF, else 0).  *px_len receives w*h*channels. */
+int nice_decode(const uint8_t* s, size_t len, uint8_t* px_out, size_t cap, uint32_t flags,
+                size_t* px_len);
+
+/* ---- context API: device buffers, HIP streams (passed as void*), batches ---- */
+int nice_ctx_create(int device, nice_ctx** out);
+void nice_ctx_destroy(nice_ctx* ctx);
+/* Pre-size scratch so later batch calls allocate nothing (graph-capturable). */
+int nice_ctx_reserve(nice_ctx* ctx, uint32_t n_frames, uint32_t w, uint32_t h);
+
+/* Encode n_frames same-shape frames resident in device memory.
+ * d_px: frame f at d_px + f*frame_stride (4-byte aligned for channels == 4).
+ * d_out: frame f's stream at d_out + f*out_stride (4-byte aligned, out_stride a
+ * multiple of 4 and >= nice_encode_bound(w, h)); d_out_len[f] = its length.
+ * Asynchronous on `stream`. */
+int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t frame_stride,
+                          uint32_t n_frames, uint32_t w, uint32_t h, uint8_t channels,
+                          uint8_t channels_out, uint8_t* d_out, uint64_t out_stride,
+                          uint64_t* d_out_len);
+
+/* Decode n_frames streams resident in device memory (all w x h).
+ * d_streams: stream f at d_streams + f*stream_stride, d_stream_len[f] bytes.
+ * d_px: frame f written at d_px + f*px_stride with out_channels (3 or 4) bytes
+ * per pixel.  d_status[f] = NICE_OK or a negative code.  Asynchronous. */
+int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
+                          uint64_t stream_stride, const uint64_t* d_stream_len, uint32_t n_frames,
+                          uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
+                          uint64_t px_stride, uint32_t flags, int32_t* d_status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NICE_H */

@@ -94,10 +94,13 @@ static void bw_write_24bits(bitwriter_t *b, uint8_t amount, uint32_t value) {
 typedef struct {
     const uint8_t *p; size_t len, pos;
     uint8_t bit_offset; uint32_t cache; uint8_t buffer;
+    size_t stale;   /* bytes "read" past the end (stale buffer reuse) */
+    int hung;       /* the reference refill loop would never terminate */
 } bitreader_t;
 
 static void br_init(bitreader_t *r, const uint8_t *p, size_t len, size_t pos) {
     r->p = p; r->len = len; r->pos = pos; r->bit_offset = 32; r->cache = 0; r->buffer = 0;
+    r->stale = 0; r->hung = 0;
 }
 
 /* bitreader.rs:31-54: read_exact of one byte (EOF -> Err -> the caller's
@@ -133,7 +136,14 @@ static uint32_t br_read_24bits(bitreader_t *r, uint8_t amount) {
 static uint32_t br_read_24bits_noclear(bitreader_t *r, uint8_t amount) {
     uint8_t aob_rev = (uint8_t)(32 - amount);
     while (r->bit_offset > aob_rev) {
+        if (r->bit_offset < 8) {
+            /* u8 `bit_offset -= 8` wraps (release build): the refill loop then
+             * cycles through one residue class mod 8 and never terminates. */
+            r->hung = 1;
+            return 0;
+        }
         if (r->pos < r->len) r->buffer = r->p[r->pos++];
+        else r->stale++;
         r->bit_offset = (uint8_t)(r->bit_offset - 8);
         r->cache = shl32(r->cache, 8) + (uint32_t)r->buffer;
     }
@@ -491,6 +501,21 @@ static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
     for (int i = 0; i < n; ++i) {
         if (br_read_bitsu8(r, fb, &a[i])) { free(a); free(code); return NICE_ORACLE_E_PANIC; }
     }
+    /* Domain check (DESIGN.md "decode domain"): a complete canonical code whose
+     * longest length equals the 5-bit max.  Every stream the reference encoder
+     * writes without a header spill satisfies it; outside it the reference fills
+     * a 2^max table with overlapping/missing entries (and may allocate GiBs). */
+    {
+        uint64_t kraft = 0; uint8_t seen = 0; int ok = mx >= 1 && mx <= 31;
+        for (int i = 0; i < n && ok; ++i) {
+            if (a[i] < 1 || a[i] > mx) ok = 0;
+            else { kraft += (uint64_t)1 << (mx - a[i]); if (a[i] > seen) seen = a[i]; }
+        }
+        if (!ok || seen != mx || kraft != ((uint64_t)1 << mx)) {
+            free(a); free(code);
+            return NICE_ORACLE_E_DOMAIN;
+        }
+    }
     nice_oracle_canonical(a, n, code);
     sl->lut_len = (size_t)1 << (mx & 63u);
     sl->lut = (lut_t *)calloc(sl->lut_len, sizeof(lut_t));
@@ -508,13 +533,52 @@ static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
     return rc;
 }
 
-static inline int read_next_symbol(bitreader_t *r, const sslookup_t *sl, unsigned *sym) {
-    uint32_t v = br_read_24bits_noclear(r, sl->max_aob);
+/* Absolute-position reader with the same byte semantics (bytes past the end
+ * read as the last stream byte) but no u32 cache: what the reference reader
+ * computes whenever it terminates.  Used by NICE_ORACLE_DEC_STRIDE ("intent"). */
+static uint32_t abs_peek(const uint8_t *p, size_t len, uint64_t bitpos, unsigned m) {
+    uint64_t acc = 0;
+    size_t b = (size_t)(bitpos >> 3);
+    for (int k = 0; k < 8; ++k) {
+        size_t i = b + (size_t)k;
+        uint8_t v = i < len ? p[i] : (len ? p[len - 1] : 0);
+        acc = (acc << 8) | v;
+    }
+    acc <<= (bitpos & 7);
+    return m ? (uint32_t)(acc >> (64 - m)) : 0u;
+}
+
+typedef struct {
+    bitreader_t r;       /* reference reader (cache + bit_offset) */
+    int intent;          /* 1: absolute reader */
+    uint64_t bitpos;     /* intent reader position */
+} symreader_t;
+
+static inline int read_next_symbol_x(symreader_t *sr, const sslookup_t *sl, unsigned *sym) {
+    uint32_t v;
+    if (sr->intent) {
+        v = abs_peek(sr->r.p, sr->r.len, sr->bitpos, sl->max_aob);
+    } else {
+        /* Past the end the reference keeps shifting in its stale byte; a run-digit
+         * pattern there never terminates (or overruns the output): report it. */
+        if (sr->r.stale > 64) return NICE_ORACLE_E_PANIC;
+        v = br_read_24bits_noclear(&sr->r, sl->max_aob);
+        if (sr->r.hung) return NICE_ORACLE_E_HANG;
+    }
     if (v >= sl->lut_len) return NICE_ORACLE_E_PANIC;
     lut_t l = sl->lut[v];
-    r->bit_offset = (uint8_t)(r->bit_offset + l.aob);
+    if (sr->intent) sr->bitpos += l.aob;
+    else sr->r.bit_offset = (uint8_t)(sr->r.bit_offset + l.aob);
     *sym = l.symbol;
     return 0;
+}
+
+static inline int read_next_symbol(bitreader_t *r, const sslookup_t *sl, unsigned *sym) {
+    symreader_t sr;
+    sr.r = *r; sr.intent = 0; sr.bitpos = 0;
+    int rc = read_next_symbol_x(&sr, sl, sym);
+    *r = sr.r;
+    return rc;
 }
 
 int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, size_t *out_len,
@@ -554,11 +618,16 @@ int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, si
                                 ch * 3 * (W + 1), ch * 3 * (W - 1)};
     const size_t back_ref[5] = {ch, ch * W, ch * (W - 1), 2 * ch, 2 * ch * W};
     const size_t rowb = ch * W;
-    const size_t step = (mode == NICE_ORACLE_DEC_STRIDE) ? ch : 3;     /* code.rs:659 */
-    unsigned prefix = 0, v;
-#define RS(stream, dst) do { if (read_next_symbol(&r, &L[stream], &(dst))) { rc = NICE_ORACLE_E_PANIC; goto done; } } while (0)
+    const int intent = (mode == NICE_ORACLE_DEC_STRIDE);
+    const size_t step = intent ? ch : 3;                                /* code.rs:659 */
+    symreader_t sr;
+    sr.r = r; sr.intent = intent;
+    sr.bitpos = (uint64_t)r.pos * 8 - (32u - r.bit_offset);             /* after the tables */
+    unsigned prefix = 0, v = 0;
+#define RS(stream, dst) do { int e_ = read_next_symbol_x(&sr, &L[stream], &(dst)); if (e_) { rc = e_; goto done; } } while (0)
 #define IDX(i) do { if ((i) >= image_size) { rc = NICE_ORACLE_E_PANIC; goto done; } } while (0)
     if (rc) goto done;
+    if (intent && (ch < 3)) { rc = NICE_ORACLE_E_ARG; goto done; }
     RS(S_PREFIX, prefix);                                               /* code.rs:550 */
     size_t position = 0, prev_pos = 0;
     while (position < image_size) {                                      /* code.rs:573 */
@@ -635,20 +704,26 @@ int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, si
             break;
         }
         default:
+            if (intent) { rc = NICE_ORACLE_E_PANIC; goto done; }         /* digit where a pixel starts */
             break;                                                       /* eprintln!, continue */
         }
         prev_pos = position;
         position += step;
+        /* intent: the stream ends with the last pixel (no extra prefix read) */
+        if (intent && position >= image_size) break;
         RS(S_PREFIX, prefix);                                            /* code.rs:660 */
         if (prefix >= P_RUN1 && prefix <= P_RUN1 + 7) {
             uint8_t shift = 0;
             size_t run = 0;
+            const size_t remaining = (image_size - position) / ch;
             while (prefix >= P_RUN1 && prefix <= P_RUN1 + 7) {
                 run += (size_t)(prefix - 5) << (shift & 63u);
                 shift = (uint8_t)(shift + 3);
+                if (intent && run + 1 >= remaining) break;               /* run reaches the end */
                 RS(S_PREFIX, prefix);
             }
             run += 1;
+            if (intent && run > remaining) { rc = NICE_ORACLE_E_PANIC; goto done; }
             for (size_t i = 0; i < run; ++i) {                          /* code.rs:675-678 */
                 size_t dst = position + i * ch;
                 IDX(prev_pos + 2); IDX(dst + 2);

@@ -14,7 +14,9 @@ enum {
     NICE_ORACLE_OK = 0,
     NICE_ORACLE_E_ARG = -1,
     NICE_ORACLE_E_OOM = -2,
-    NICE_ORACLE_E_PANIC = -3   /* the reference would panic (index OOB, EOF in read_exact, ...) */
+    NICE_ORACLE_E_PANIC = -3,  /* the reference would panic (index OOB, EOF in read_exact, ...) */
+    NICE_ORACLE_E_DOMAIN = -4, /* code tables outside the decodable domain (see read_header_into_tree) */
+    NICE_ORACLE_E_HANG = -5    /* the reference decoder would loop forever (bitreader.rs:88-97 u8 wrap) */
 };
 
 enum { NICE_ORACLE_DEC_REFERENCE = 0, NICE_ORACLE_DEC_STRIDE = 1 };

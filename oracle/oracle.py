@@ -18,7 +18,16 @@ _lib = None
 
 STREAM_N = [256, 13, 64, 32, 11, 343, 64, 32, 32, 11]
 DEC_REFERENCE = 0
-DEC_STRIDE = 1
+DEC_STRIDE = 1          # "intent" decode: pixel stride = channels, correct bit reader
+E_PANIC, E_DOMAIN, E_HANG = -3, -4, -5
+
+
+class OracleDecodeError(RuntimeError):
+    def __init__(self, rc):
+        self.rc = rc
+        what = {E_PANIC: "reference would panic", E_DOMAIN: "tables outside the decodable domain",
+                E_HANG: "reference decoder would never terminate"}.get(rc, "error")
+        super().__init__(f"oracle decode failed rc={rc} ({what})")
 
 
 class Stats(ctypes.Structure):
@@ -113,7 +122,7 @@ def decode(stream: bytes, mode: int = DEC_REFERENCE):
     rc = L.nice_oracle_decode(_u8p(buf), buf.size, mode, ctypes.byref(out), ctypes.byref(n),
                               ctypes.byref(w), ctypes.byref(h), ctypes.byref(ch))
     if rc != 0:
-        raise RuntimeError(f"oracle decode failed rc={rc} (reference would panic)")
+        raise OracleDecodeError(rc)
     try:
         px = np.frombuffer(ctypes.string_at(out, n.value), dtype=np.uint8).copy()
     finally:

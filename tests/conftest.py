@@ -1,0 +1,36 @@
+"""Shared test setup: markers, repo paths, and loaders for the product package
+(hyphenated directory, imported with importlib) and the oracle (checker only)."""
+import importlib
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+PKG_NAME = "fast-losless-image-compression-format_amd"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
+
+
+def nice_pkg():
+    return importlib.import_module(PKG_NAME)
+
+
+def oracle_mod():
+    from oracle import oracle as O
+    return O
+
+
+@pytest.fixture(scope="session")
+def O():
+    return oracle_mod()
+
+
+@pytest.fixture(scope="session")
+def nice():
+    return nice_pkg()

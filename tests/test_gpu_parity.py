@@ -1,0 +1,136 @@
+"""GPU parity: the HIP encoder must produce the oracle's stream byte for byte and
+the HIP decoder must reproduce the oracle's pixels, through the C ABI.
+
+Encode parity is bit-exact against the literal restatement of code::encode.
+Decode parity: against the oracle's reference-mode decode where the reference
+terminates (channels == 3, every max code length <= 24), and against the
+original pixels (and the oracle's intent-mode decode) everywhere else.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames():
+    """(name, pixels, w, h, c) cases covering the reference test surface."""
+    from conftest import oracle_mod
+    O = oracle_mod()
+    rng = np.random.default_rng(1234)
+    cases = [
+        ("syn512x4", O.gen_syn_v1(512, 512, 4, 1), 512, 512, 4),
+        ("syn256x3", O.gen_syn_v1(256, 256, 3, 1), 256, 256, 3),
+        ("syn160x120x3s4", O.gen_syn_v1(160, 120, 3, 4), 160, 120, 3),
+        ("syn1920x1080x4", O.gen_syn_v1(1920, 1080, 4, 3), 1920, 1080, 4),
+        ("grad512x4", O.gen_gradient(512, 512, 4), 512, 512, 4),
+        ("grad64x48x3", O.gen_gradient(64, 48, 3), 64, 48, 3),
+        ("odd37x23x4", O.gen_syn_v1(37, 23, 4, 9), 37, 23, 4),
+        ("wide1000x7x3", O.gen_syn_v1(1000, 7, 3, 5), 1000, 7, 3),
+        ("noise300x200x3", rng.integers(0, 256, 300 * 200 * 3, dtype=np.uint8), 300, 200, 3),
+        ("noise128x128x4", rng.integers(0, 256, 128 * 128 * 4, dtype=np.uint8), 128, 128, 4),
+        ("flat640x480x4", np.tile(np.array([9, 8, 7, 255], np.uint8), 640 * 480), 640, 480, 4),
+        ("w1", O.gen_syn_v1(1, 50, 3, 2), 1, 50, 3),
+        ("w2", O.gen_syn_v1(2, 30, 3, 2), 2, 30, 3),
+        ("w3", O.gen_syn_v1(3, 20, 4, 2), 3, 20, 4),
+        ("5x5", O.gen_syn_v1(5, 5, 3, 2), 5, 5, 3),
+        ("1x1", np.array([1, 2, 3], np.uint8), 1, 1, 3),
+    ]
+    # stripes: long runs crossing encoder tiles (1024 px) and decoder segments
+    st = np.zeros((300, 700, 3), np.uint8)
+    st[:, :, 0] = (np.arange(300)[:, None] // 7) * 20
+    st[::5, ::3, 1] = 200
+    cases.append(("stripes700x300x3", st.reshape(-1), 700, 300, 3))
+    # few colours: back references and luma references dominate
+    pal = np.array([[10, 20, 30], [10, 21, 31], [200, 100, 50], [12, 22, 29]], np.uint8)
+    idx = rng.integers(0, 4, (90, 333))
+    idx[:, 100:200] = 2
+    cases.append(("palette333x90x3", pal[idx].reshape(-1), 333, 90, 3))
+    return cases
+
+
+CASES = _frames()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_encode_bitexact(nice, O, case):
+    name, px, w, h, c = case
+    want = O.encode(px, w, h, c)
+    got = nice.encode_bytes(px, w, h, c)
+    assert len(got) == len(want), (len(got), len(want))
+    if got != want:
+        d = next(i for i in range(len(want)) if got[i] != want[i])
+        pytest.fail(f"{name}: first differing byte {d} of {len(want)}")
+
+
+def test_encode_empty(nice, O):
+    for w, h in [(0, 0), (7, 0), (0, 5)]:
+        px = np.zeros(0, np.uint8)
+        assert nice.encode_bytes(px, w, h, 4) == O.encode(px, w, h, 4)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_decode_matches(nice, O, case):
+    name, px, w, h, c = case
+    s = O.encode(px, w, h, c)
+    rgb = px.reshape(-1, c)[:, :3].reshape(-1)
+    try:
+        got, img = nice.decode_bytes(s)
+    except nice.NiceError as e:
+        # only streams outside the decodable domain may be refused
+        with pytest.raises(O.OracleDecodeError):
+            O.decode(s, O.DEC_STRIDE)
+        return
+    assert (img.width, img.height, img.channels) == (w, h, c)
+    g = np.frombuffer(got, np.uint8).reshape(-1, c)
+    assert np.array_equal(g[:, :3].reshape(-1), rgb), name
+    if c == 4:
+        assert (g[:, 3] == 255).all()
+    ref, _ = O.decode(s, O.DEC_STRIDE)
+    assert np.array_equal(np.frombuffer(got, np.uint8), ref.reshape(-1, c).reshape(-1)[:len(got)]) or c == 4
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[4] == 3], ids=[c[0] for c in CASES if c[4] == 3])
+def test_decode_strict_reference(nice, O, case):
+    """STRICT_REFERENCE: fail exactly where the literal reference fails (or may not
+    terminate); otherwise identical pixels."""
+    name, px, w, h, c = case
+    s = O.encode(px, w, h, c)
+    try:
+        ref, _ = O.decode(s)
+        ref_ok = True
+    except O.OracleDecodeError:
+        ref_ok = False
+    try:
+        got, _ = nice.decode_bytes(s, flags=nice.DEC_STRICT_REFERENCE)
+        ok = True
+    except nice.NiceError:
+        ok = False
+    if ref_ok and ok:
+        assert np.array_equal(np.frombuffer(got, np.uint8), ref)
+    else:
+        # strict mode is conservative on max length > 24; never accepts what the reference rejects
+        assert not ok or ref_ok
+
+
+def test_batch_device_roundtrip(nice, O):
+    import torch
+    w, h, c, n = 640, 360, 4, 6
+    frames = np.stack([O.gen_syn_v1(w, h, c, s) for s in range(1, n + 1)])
+    px = torch.from_numpy(frames).cuda()
+    bound = (nice.encode_bound(w, h) + 255) // 256 * 256
+    out = torch.zeros((n, bound), dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(n, dtype=torch.int64, device="cuda")
+    nice.encode_batch(px, w, h, c, out, lens)
+    torch.cuda.synchronize()
+    L = lens.cpu().numpy()
+    for i in range(n):
+        want = O.encode(frames[i], w, h, c)
+        assert L[i] == len(want)
+        assert bytes(out[i, :L[i]].cpu().numpy()) == want
+    dec = torch.zeros((n, w * h * 4), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(n, dtype=torch.int32, device="cuda")
+    nice.decode_batch(out, lens, w, h, 4, dec, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    got = dec.cpu().numpy().reshape(n, -1, 4)
+    assert np.array_equal(got[:, :, :3], frames.reshape(n, -1, 4)[:, :, :3])
