@@ -63,6 +63,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise NiceError(E_NODEV, f"{LIB_PATH} missing (run __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7; load it
+    # first so libnice_hip.so binds to the same runtime (same SONAME) and device
+    # pointers / streams are shared with torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     u8p = ctypes.c_void_p
     sz = ctypes.c_size_t
