@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: NICE2 encode+decode of 4K RGBA frames resident in HBM.
+
+One "step" encodes a batch of F synthetic 3840x2160 RGBA frames on the GPU and
+decodes the resulting streams back (steady-state throughput of repeated frames,
+SURVEY.md §8d; BASELINE.json metric "encode+decode MPixels/s on 4K RGBA").
+Frames are independent, so N GPUs shard frames with no collective ("weak").
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP
+events around its launches inside the timed region; algorithmic bytes per
+launch) and the CPU baseline (the oracle restatement of the
+reference, single thread, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "fast-losless-image-compression-format_amd"
+
+HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+AMP = [0, 1, 2, 3, 8, 24, 64, 256]
+
+
+def syn_frames(torch, n, W, H, seed0, device):
+    """Photo-like RGBA frames (SYN-v1 structure with a counter-based hash in
+    place of the serial xorshift): per-band noise amplitudes 0..256, 1/7 of the
+    16x16 blocks flat, A = 255."""
+    y = torch.arange(H, device=device, dtype=torch.int64).view(H, 1)
+    x = torch.arange(W, device=device, dtype=torch.int64).view(1, W)
+    bx = (200 * x) // max(W - 1, 1)
+    by = (200 * y) // max(H - 1, 1)
+    base = [bx.expand(H, W), by.expand(H, W), ((bx + by) // 2)]
+    flat = (((x // 16) + (y // 16)) % 7) == 0
+    amp = torch.tensor(AMP, device=device, dtype=torch.int64)[(8 * y) // H].expand(H, W)
+    idx = y * W + x
+    out = torch.empty((n, H, W, 4), dtype=torch.uint8, device=device)
+    M = 0xFFFFFFFF
+    for f in range(n):
+        for c in range(3):
+            v = (idx * 2654435761 + (seed0 + f) * 40503 + c * 977) & M
+            v = v ^ (v >> 16)
+            v = (v * 0x7FEB352D) & M
+            v = v ^ (v >> 15)
+            v = (v * 0x846CA68B) & M
+            v = v ^ (v >> 16)
+            a = amp.clamp(min=1)
+            noise = torch.where(amp == 0, torch.zeros_like(v),
+                                torch.where(amp < 256, (v % a) - amp // 2, v & 255))
+            val = (base[c] + noise) % 256
+            fv = [40, 80, 120][c]
+            out[f, :, :, c] = torch.where(flat, torch.full_like(val, fv), val).to(torch.uint8)
+        out[f, :, :, 3] = 255
+    return out.view(n, H * W * 4)
+
+
+def cpu_baseline(W, H, seconds=12.0):
+    """Oracle (C restatement of the reference, -O3, 1 thread): encode + decode of
+    4K RGBA frames until ~`seconds` of CPU work.  Decode runs on the stream's
+    channels=3 view (byte 12 patched), the only form the reference decodes."""
+    from oracle import oracle as O
+    n = 0
+    t_total = 0.0
+    seed = 1
+    while t_total < seconds and n < 64:
+        px = O.gen_syn_v1(W, H, 4, seed)
+        t0 = time.perf_counter()
+        s = O.encode(px, W, H, 4)
+        s3 = bytearray(s)
+        s3[12] = 3
+        O.decode(bytes(s3))
+        t_total += time.perf_counter() - t0
+        n += 1
+        seed += 1
+    return {"value": round(n * W * H / t_total / 1e6, 3), "unit": "MPixels/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{n} x {W}x{H} RGBA NICE-SYN-v1 frames (seeds 1..{n}), encode+decode, "
+                      f"{t_total:.1f} s single-thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    nice = importlib.import_module(PKG)
+    L = nice.lib()
+    L.nice_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.nice_ctx_read_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_uint32)]
+    L.nice_phase_name.restype = ctypes.c_char_p
+
+    W, H, F = args.width, args.height, args.frames
+    N = W * H
+    px = syn_frames(torch, F, W, H, seed0=1 + rank * F, device=device)
+    stride = (nice.encode_bound(W, H) + 255) // 256 * 256
+    streams = torch.empty((F, stride), dtype=torch.uint8, device=device)
+    lens = torch.zeros(F, dtype=torch.int64, device=device)
+    dec = torch.empty((F, N * 4), dtype=torch.uint8, device=device)
+    status = torch.zeros(F, dtype=torch.int32, device=device)
+    ctx = nice._ctx(local)
+
+    def step():
+        nice.encode_batch(px, W, H, 4, streams, lens)
+        nice.decode_batch(streams, lens, W, H, 4, dec, status)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness of the measured work (outside the timed region)
+    assert int(status.abs().sum()) == 0, "decode reported an error"
+    assert torch.equal(dec.view(F, N, 4)[:, :, :3], px.view(F, N, 4)[:, :, :3]), "round trip mismatch"
+    stream_bytes = int(lens.sum())
+
+    L.nice_ctx_set_timing(ctx.ptr, 1)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms = (ctypes.c_double * 12)()
+    cnt = (ctypes.c_uint32 * 12)()
+    L.nice_ctx_read_timing(ctx.ptr, ms, cnt)
+    L.nice_ctx_set_timing(ctx.ptr, 0)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # encode-only / decode-only rates (separate short runs, outside the main timing)
+    def timed(fn, reps=2):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps
+    t_enc = timed(lambda: nice.encode_batch(px, W, H, 4, streams, lens))
+    t_dec = timed(lambda: nice.decode_batch(streams, lens, W, H, 4, dec, status))
+    # single-frame latency (one 4K frame, encode then decode)
+    one_px, one_s, one_l = px[:1], streams[:1], lens[:1]
+    one_d, one_st = dec[:1], status[:1]
+    t_one = timed(lambda: (nice.encode_batch(one_px, W, H, 4, one_s, one_l),
+                           nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st)), reps=2)
+
+    names = [L.nice_phase_name(i).decode() for i in range(12)]
+    phase = {names[i]: {"ms_total": round(ms[i], 3), "launches": int(cnt[i])}
+             for i in range(12) if cnt[i]}
+    # dominant kernel and its algorithmic bytes per launch
+    in_bytes = F * N * 4
+    out_px_bytes = F * N * 4
+    algo = {
+        "enc_classify": in_bytes, "enc_pack": in_bytes + stream_bytes,
+        "dec_sync": stream_bytes, "dec_count": stream_bytes, "dec_bounds": stream_bytes,
+        "dec_reconstruct": stream_bytes + out_px_bytes,
+    }
+    dom = max((k for k in phase if k in algo), key=lambda k: phase[k]["ms_total"])
+    avg_s = phase[dom]["ms_total"] / 1e3 / phase[dom]["launches"]
+    achieved = algo[dom] / avg_s / 1e9
+    total_px = N * F * args.steps * world
+    value = total_px / elapsed / 1e6
+    res = {
+        "metric": "encode+decode MPixels/s on 4K RGBA at 1/2/4/8 MI355X; bitstream bit-exact",
+        "value": round(value, 3),
+        "unit": "MPixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SYN-v1-structured photo-like RGBA frames generated on device)",
+        "config": {"workload": f"{F} x {W}x{H} RGBA frames per GPU per step, encode then decode, "
+                               f"inputs resident in HBM", "width": W, "height": H,
+                   "channels": 4, "frames_per_gpu_per_step": F,
+                   "parallelism": f"frames sharded over {world} GPU(s), no collective"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": round(achieved * 1e9 / HBM_PEAK, 5), "traffic": None,
+                     "algo_bytes_per_launch": algo[dom],
+                     "avg_launch_ms": round(avg_s * 1e3, 4)},
+        "encode_mpix_s": round(F * N / t_enc / 1e6, 2),
+        "decode_mpix_s": round(F * N / t_dec / 1e6, 2),
+        "single_frame_latency_ms": round(t_one * 1e3, 2),
+        "stream_bytes_per_frame": stream_bytes // F,
+        "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
+        "phase_ms_timed_region": phase,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(W, H, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -89,10 +89,49 @@ int check_device(int device) {
 
 }  // namespace
 
+static const char* kPhaseNames[NICE_PHASES] = {
+    "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_pack", "enc_serial",
+    "dec_tables", "dec_sync", "dec_count", "dec_scan", "dec_bounds", "dec_reconstruct"};
+
+// Optional per-phase HIP-event timing (bench / profiling).
+struct PhaseTimer {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  struct Mark { int phase; hipEvent_t a, b; };
+  std::vector<Mark> marks;
+  hipEvent_t take() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  void begin(int phase, hipStream_t st) {
+    if (!on) return;
+    Mark m{phase, take(), take()};
+    if (!m.a || !m.b) return;
+    (void)hipEventRecord(m.a, st);
+    marks.push_back(m);
+  }
+  void end(hipStream_t st) {
+    if (!on || marks.empty()) return;
+    (void)hipEventRecord(marks.back().b, st);
+  }
+  void release() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+    marks.clear();
+    used = 0;
+  }
+};
+
 struct nice_ctx {
   int device = 0;
   std::mutex mu;
   Arena enc, dec, host_px, host_out, dev_len;
+  PhaseTimer timer;
 };
 
 extern "C" {
@@ -140,6 +179,7 @@ void nice_ctx_destroy(nice_ctx* ctx) {
   ctx->host_px.release();
   ctx->host_out.release();
   ctx->dev_len.release();
+  ctx->timer.release();
   (void)hipSetDevice(prev);
   delete ctx;
 }
@@ -216,14 +256,27 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     if (per < 1) per = 1;
     blocks = (total_tiles + per - 1) / per;
     a.tiles_per_block = (uint32_t)per;
+    PhaseTimer& tm = ctx->timer;
+    tm.begin(NICE_PH_ENC_CLASSIFY, st);
     hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    tm.end(st);
+    tm.begin(NICE_PH_ENC_TAILRUNS, st);
     hipLaunchKernelGGL(enc_tailruns, dim3(n_frames), dim3(1024), 0, st, a);
+    tm.end(st);
   }
+  ctx->timer.begin(NICE_PH_ENC_TABLES, st);
   hipLaunchKernelGGL(enc_tables, dim3(n_frames * N_STREAMS), dim3(64), 0, st, a);
+  ctx->timer.end(st);
+  ctx->timer.begin(NICE_PH_ENC_HEADER, st);
   hipLaunchKernelGGL(enc_header, dim3(n_frames), dim3(64), 0, st, a);
+  ctx->timer.end(st);
   if (T > 0) {
+    ctx->timer.begin(NICE_PH_ENC_PACK, st);
     hipLaunchKernelGGL(enc_pack, dim3((uint32_t)total_tiles), dim3(256), 0, st, a);
+    ctx->timer.end(st);
+    ctx->timer.begin(NICE_PH_ENC_SERIAL, st);
     hipLaunchKernelGGL(enc_serial, dim3(n_frames), dim3(64), 0, st, a);
+    ctx->timer.end(st);
   }
   NICE_HIP(hipGetLastError());
   return NICE_OK;
@@ -381,7 +434,10 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   ParseState* eb = (ParseState*)(base + L.o_eb);
   uint32_t* changed = (uint32_t*)(base + L.o_changed);
 
+  PhaseTimer& tm = ctx->timer;
+  tm.begin(NICE_PH_DEC_TABLES, st);
   hipLaunchKernelGGL(dec_tables, dim3(n_frames), dim3(256), 0, st, a);
+  tm.end(st);
   if (N == 0) {
     NICE_HIP(hipGetLastError());
     return NICE_OK;
@@ -393,22 +449,62 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   uint32_t host_changed = 1;
   for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it) {
     NICE_HIP(hipMemsetAsync(changed, 0, 4, st));
+    tm.begin(NICE_PH_DEC_SYNC, st);
     hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, (const ParseState*)ea, eb, changed);
+    tm.end(st);
     NICE_HIP(hipMemcpyAsync(&host_changed, changed, 4, hipMemcpyDeviceToHost, st));
     NICE_HIP(hipStreamSynchronize(st));
     ParseState* t = ea;
     ea = eb;
     eb = t;
   }
+  tm.begin(NICE_PH_DEC_COUNT, st);
   hipLaunchKernelGGL(dec_count, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  tm.end(st);
+  tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
+  tm.end(st);
+  tm.begin(NICE_PH_DEC_BOUNDS, st);
   hipLaunchKernelGGL(dec_bounds, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  tm.end(st);
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+  tm.begin(NICE_PH_DEC_RECON, st);
   hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
+  tm.end(st);
   NICE_HIP(hipGetLastError());
   return NICE_OK;
+}
+
+int nice_ctx_set_timing(nice_ctx* ctx, int on) {
+  if (!ctx) return NICE_E_ARG;
+  ctx->timer.on = on != 0;
+  ctx->timer.marks.clear();
+  ctx->timer.used = 0;
+  return NICE_OK;
+}
+
+int nice_ctx_read_timing(nice_ctx* ctx, double* ms, uint32_t* count) {
+  if (!ctx || !ms) return NICE_E_ARG;
+  for (int i = 0; i < NICE_PHASES; ++i) {
+    ms[i] = 0.0;
+    if (count) count[i] = 0;
+  }
+  for (auto& m : ctx->timer.marks) {
+    if (hipEventSynchronize(m.b) != hipSuccess) return NICE_E_HIP;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, m.a, m.b) != hipSuccess) return NICE_E_HIP;
+    ms[m.phase] += t;
+    if (count) count[m.phase] += 1;
+  }
+  ctx->timer.marks.clear();
+  ctx->timer.used = 0;
+  return NICE_OK;
+}
+
+const char* nice_phase_name(int phase) {
+  return (phase >= 0 && phase < NICE_PHASES) ? kPhaseNames[phase] : "";
 }
 
 int nice_decode(const uint8_t* s, size_t len, uint8_t* px_out, size_t cap, uint32_t flags,

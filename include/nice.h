@@ -88,6 +88,17 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                           uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
                           uint64_t px_stride, uint32_t flags, int32_t* d_status);
 
+/* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
+enum {
+  NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,
+  NICE_PH_ENC_PACK, NICE_PH_ENC_SERIAL, NICE_PH_DEC_TABLES, NICE_PH_DEC_SYNC, NICE_PH_DEC_COUNT,
+  NICE_PH_DEC_SCAN, NICE_PH_DEC_BOUNDS, NICE_PH_DEC_RECON, NICE_PHASES
+};
+int nice_ctx_set_timing(nice_ctx* ctx, int on);
+/* Sums (ms) and launch counts per phase since the last read; synchronises. */
+int nice_ctx_read_timing(nice_ctx* ctx, double* ms, uint32_t* count);
+const char* nice_phase_name(int phase);
+
 #ifdef __cplusplus
 }
 #endif
