@@ -16,13 +16,15 @@
 
 namespace nice {
 
-constexpr int DEC_LUT_BITS = 9;
-constexpr int DEC_LUT_PER_STREAM = 1 << DEC_LUT_BITS;
+constexpr int DEC_LUT_MAX_BITS = 12;      // per stream first-level width cap
+constexpr int DEC_LUT_BUDGET = 12288;     // entries over all 10 streams (24 KiB)
 
 // Per-frame decode tables (global memory; copied to LDS by the kernels).
 struct DecTables {
-  // first level: (symbol << 5) | length, length == 0 => long code
-  uint16_t lut[N_STREAMS][DEC_LUT_PER_STREAM];
+  // first level: (symbol << 5) | length, length == 0 => long code; stream s
+  // occupies lut[lut_off[s] .. lut_off[s] + 2^lut_bits[s])
+  uint16_t lut[DEC_LUT_BUDGET];
+  uint16_t lut_off[N_STREAMS];
   // canonical order per stream: aligned lower bound (code << (max - len)),
   // symbol and length, in (len desc, symbol desc) order
   uint32_t lo[N_BINS];
@@ -61,7 +63,7 @@ template <class Tab>
 __device__ __forceinline__ uint32_t dec_symbol(const BitSrc& src, const Tab& t, int s, uint64_t* pos) {
   const uint32_t v = src.peek32(*pos);
   const uint32_t lb = t.lut_bits[s];
-  const uint32_t e = t.lut[s][v >> (32 - lb)];
+  const uint32_t e = t.lut[t.lut_off[s] + (v >> (32 - lb))];
   if (e & 31u) {
     *pos += e & 31u;
     return e >> 5;

@@ -2,6 +2,8 @@
 // kernel launch sequences and the host-buffer convenience entry points.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -91,7 +93,7 @@ int check_device(int device) {
 
 static const char* kPhaseNames[NICE_PHASES] = {
     "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_pack", "enc_serial",
-    "dec_tables", "dec_sync", "dec_count", "dec_scan", "dec_bounds", "dec_reconstruct"};
+    "dec_tables", "dec_sync", "dec_count", "dec_scan", "dec_emit", "dec_reconstruct"};
 
 // Optional per-phase HIP-event timing (bench / profiling).
 struct PhaseTimer {
@@ -287,9 +289,9 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
 namespace {
 struct DecLayout {
   size_t total;
-  size_t o_tables, o_dstart, o_ea, o_eb, o_cpx, o_cstart, o_bounds, o_changed, o_rowbuf;
+  size_t o_tables, o_dstart, o_ea, o_eb, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
 };
-DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t H, uint32_t nseg, size_t rowbuf) {
+DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint64_t npx, size_t rowbuf) {
   DecLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -299,7 +301,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t H, uint32_
   L.o_eb = take((size_t)n_frames * max_chunks * sizeof(ParseState));
   L.o_cpx = take((size_t)n_frames * max_chunks * 8);
   L.o_cstart = take((size_t)n_frames * max_chunks * 8);
-  L.o_bounds = take((size_t)n_frames * H * nseg * sizeof(SegBound));
+  L.o_recs = take((size_t)n_frames * npx * 4);
   L.o_changed = take(16);
   L.o_rowbuf = take(rowbuf);
   L.total = o;
@@ -318,7 +320,7 @@ RecGeom rec_geom(uint32_t w) {
   g.nseg = w ? (w + s - 1) / s : 1;
   g.R = w >= 3 ? 4 : 8;
   const size_t kw = (w + 31) / 32;
-  const size_t head = align_up((sizeof(DecTables) + 7 * 4), 16) + align_up(kw, 4) * 4;
+  const size_t head = 512 + align_up(kw, 4) * 4 + align_up(w, 4) * 4;   // RecLds <= 512 B
   const size_t ring = (size_t)g.R * w * 4;
   g.in_lds = head + ring <= 150 * 1024;
   g.lds = g.in_lds ? head + ring : head;
@@ -403,7 +405,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
       max_len * 8 > D ? (uint32_t)((max_len * 8 - D + DEC_CHUNK_BITS - 1) / DEC_CHUNK_BITS) : 1;
   const RecGeom g = rec_geom(w);
   const size_t rowbuf = g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4;
-  DecLayout L = dec_layout(n_frames, max_chunks, h, g.nseg, rowbuf);
+  DecLayout L = dec_layout(n_frames, max_chunks, N, rowbuf);
   int rc = ctx->dec.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->dec.ptr;
@@ -425,7 +427,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   a.chunk_blocks = (max_chunks + 255) / 256;
   a.chunk_px = (unsigned long long*)(base + L.o_cpx);
   a.chunk_start = (unsigned long long*)(base + L.o_cstart);
-  a.bounds = base + L.o_bounds;
+  a.recs = (uint32_t*)(base + L.o_recs);
   a.seg = g.seg;
   a.nseg = g.nseg;
   a.rows_in_lds = g.in_lds ? 1u : 0u;
@@ -447,7 +449,8 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   const dim3 cgrid(n_frames * a.chunk_blocks);
   // Jacobi iteration of the chunk entry states to the fixpoint
   uint32_t host_changed = 1;
-  for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it) {
+  uint32_t it_count = 0;
+  for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it, ++it_count) {
     NICE_HIP(hipMemsetAsync(changed, 0, 4, st));
     tm.begin(NICE_PH_DEC_SYNC, st);
     hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, (const ParseState*)ea, eb, changed);
@@ -465,14 +468,31 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
   tm.begin(NICE_PH_DEC_BOUNDS, st);
-  hipLaunchKernelGGL(dec_bounds, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  NICE_HIP(hipMemsetAsync(a.recs, 0xFF, (size_t)n_frames * N * 4, st));   // REC_RUN fill
+  hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
   tm.end(st);
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
+  unsigned long long* dstats = nullptr;
+  if (want_stats && hipMalloc(&dstats, 64) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 64, st);
+    a.stats = dstats;
+  }
   tm.begin(NICE_PH_DEC_RECON, st);
   hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
   tm.end(st);
+  if (dstats) {
+    unsigned long long h[8] = {0};
+    (void)hipMemcpyAsync(h, dstats, 64, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    fprintf(stderr,
+            "[nice dec stats] rows=%llu unconverged_segs=%llu tail_unknown_segs=%llu "
+            "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u\n",
+            h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg);
+    (void)hipFree(dstats);
+  }
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }

@@ -123,13 +123,35 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     }
   }
   __syncthreads();
+  __shared__ uint8_t lbits[N_STREAMS];
+  __shared__ uint16_t loff[N_STREAMS];
+  if (threadIdx.x == 0) {
+    // first-level widths: the full max length where possible, shrinking the
+    // widest tables until all ten fit the budget (long codes take the search)
+    uint32_t tot = 0;
+    for (int st = 0; st < N_STREAMS; ++st) {
+      lbits[st] = (uint8_t)min((uint32_t)smax[st], (uint32_t)DEC_LUT_MAX_BITS);
+      tot += 1u << lbits[st];
+    }
+    while (tot > (uint32_t)DEC_LUT_BUDGET) {
+      int w = 0;
+      for (int st = 1; st < N_STREAMS; ++st) if (lbits[st] > lbits[w]) w = st;
+      tot -= 1u << (lbits[w] - 1);
+      lbits[w] -= 1;
+    }
+    uint32_t o = 0;
+    for (int st = 0; st < N_STREAMS; ++st) { loff[st] = (uint16_t)o; o += 1u << lbits[st]; }
+  }
+  __syncthreads();
   if (threadIdx.x < N_STREAMS) {
     const int st = threadIdx.x;
     const int n = stream_size(st), b = stream_base(st);
     const uint32_t mx = smax[st];
-    const uint32_t lb = mx < (uint32_t)DEC_LUT_BITS ? mx : (uint32_t)DEC_LUT_BITS;
+    const uint32_t lb = lbits[st];
+    uint16_t* lut = T->lut + loff[st];
     T->max_aob[st] = (uint8_t)mx;
     T->lut_bits[st] = (uint8_t)lb;
+    T->lut_off[st] = loff[st];
     unsigned long long cur = 0;
     uint32_t prev = 0;
     for (int k = 0; k < n; ++k) {
@@ -145,9 +167,9 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
       // first-level entries
       if (l <= lb) {
         const uint32_t e0 = code << (lb - l), e1 = (code + 1) << (lb - l);
-        for (uint32_t e = e0; e < e1; ++e) T->lut[st][e] = (uint16_t)((sym << 5) | l);
+        for (uint32_t e = e0; e < e1; ++e) lut[e] = (uint16_t)((sym << 5) | l);
       } else {
-        T->lut[st][code >> (l - lb)] = 0;   // long-code marker
+        lut[code >> (l - lb)] = 0;   // long-code marker
       }
     }
   }
@@ -315,37 +337,60 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// D4: parse state at row-segment starts.  bounds[y*nseg + s] = {pos, run}:
-// run > 0: the segment starts with `run` copies of its left neighbour, then the
-// next coded pixel's prefix is at pos; run == 0: a coded pixel's prefix at pos.
+// D4: per-pixel records.  With every chunk's entry state and first pixel index
+// known, each chunk decodes its symbols again and writes one 32-bit record per
+// coded pixel; run pixels keep the REC_RUN fill.  A record says how the pixel
+// follows from already decoded pixels (code.rs:579-644):
+//   value_c = src_c + c_c (mod 256), c = bits 0..23,
+//   src = floor((L + U) / 2) (L on row 0)      kind AVG: SMALL_DIFF, LUMA2, RGB
+//   src = pixel i - off(refid)                 kind REF: BACK_REF (refid 0..4),
+//                                                        LUMA (refid 5..15)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void put_bound(const DecArgs& a, uint64_t fb, uint64_t b, uint64_t pos,
-                                          uint64_t run) {
-  const uint64_t y = b / a.W, x = b - y * a.W;
-  if (x % a.seg != 0) return;
-  SegBound* B = reinterpret_cast<SegBound*>(a.bounds) + fb + y * a.nseg + x / a.seg;
-  B->pos = pos;
-  B->run = run;
-}
+constexpr uint32_t REC_RUN = 0xFFFFFFFFu;
+constexpr uint32_t REC_REF = 1u << 28;
+__host__ __device__ constexpr int ref_rows(int id) { return id < 5 ? br_rows(id) : lr_rows(id - 5); }
+__host__ __device__ constexpr int ref_px_off(int id) { return id < 5 ? br_px(id) : lr_px(id - 5); }
 
-__device__ inline void put_run_bounds(const DecArgs& a, uint64_t fb, uint64_t first, uint64_t endx,
-                                      uint64_t pos) {
-  // boundaries b in [first, endx): run remaining = endx - b
-  uint64_t y = first / a.W;
-  for (; y * a.W < endx; ++y) {
-    const uint64_t row0 = y * a.W;
-    uint64_t xlo = first > row0 ? first - row0 : 0;
-    const uint64_t xhi = min((uint64_t)a.W, endx - row0);
-    uint64_t s = (xlo + a.seg - 1) / a.seg;
-    for (uint64_t x = s * a.seg; x < xhi; x += a.seg) {
-      SegBound* B = reinterpret_cast<SegBound*>(a.bounds) + fb + y * a.nseg + x / a.seg;
-      B->pos = pos;
-      B->run = endx - (row0 + x);
+__device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_t mode, uint32_t s0,
+                                           uint32_t s1, uint32_t s2, uint32_t s3, uint32_t* rec) {
+  const uint64_t W = a.W;
+  const uint64_t y = q / W;
+  switch (mode) {
+    case P_BACK_REF:
+    case P_LUMA: {
+      const uint32_t id = mode == P_BACK_REF ? s0 : 5u + s0;
+      if ((mode == P_BACK_REF && s0 >= 5) || (mode == P_LUMA && s0 >= 11)) return NICE_E_FORMAT;
+      const int64_t off = (int64_t)ref_rows((int)id) * (int64_t)W + ref_px_off((int)id);
+      // usize wrap (W < 3) or underflow before the image: the reference panics
+      if (off < 0 || (int64_t)q < off) return NICE_E_FORMAT;
+      uint32_t c = 0;
+      if (mode == P_LUMA) {
+        const uint32_t g = (s1 - 32u) & 255u;
+        c = ((s2 - 16u + g) & 255u) | (g << 8) | (((s3 - 16u + g) & 255u) << 16);
+      }
+      *rec = REC_REF | (id << 24) | c;
+      return 0;
     }
+    case P_SMALL_DIFF: {
+      const uint32_t rd = s0 % 7, t1 = s0 / 7;
+      *rec = ((rd - 3u) & 255u) | ((((t1 % 7) - 3u) & 255u) << 8) | ((((t1 / 7) - 3u) & 255u) << 16);
+      return 0;
+    }
+    case P_LUMA2: {
+      if (y == 0) return NICE_E_FORMAT;   // position - channels*width underflows (code.rs:583)
+      const uint32_t g = (s0 - 32u) & 255u;
+      *rec = ((s1 - 16u + g) & 255u) | (g << 8) | (((s2 - 16u + g) & 255u) << 16);
+      return 0;
+    }
+    case P_RGB:
+      *rec = (s0 & 255u) | ((s1 & 255u) << 8) | ((s2 & 255u) << 16);
+      return 0;
+    default:
+      return NICE_E_FORMAT;
   }
 }
 
-__global__ __launch_bounds__(256) void dec_bounds(DecArgs a, const ParseState* entry) {
+__global__ __launch_bounds__(256) void dec_emit(DecArgs a, const ParseState* entry) {
   __shared__ DecTables T;
   const uint32_t f = blockIdx.x / a.chunk_blocks;
   const uint32_t jb = blockIdx.x % a.chunk_blocks;
@@ -367,345 +412,287 @@ __global__ __launch_bounds__(256) void dec_bounds(DecArgs a, const ParseState* e
   if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
   const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
   const uint64_t hard = len * 8 + 64;
-  const uint64_t fb = (uint64_t)f * a.H * a.nseg;
+  uint32_t* rec = a.recs + (uint64_t)f * N;
   const bool strict = (a.flags & NICE_DEC_STRICT_REFERENCE) != 0;
-  // a run whose digits brought the count to N was closed by the chunk that read them
-  bool closed = (q == N);
+  // the pixel whose payload straddles our entry belongs to the previous chunk
+  while (ps.g != 0 && ps.pos < hard) { uint64_t px = 0; parse_step(src, T, ps, px); }
+  bool closed = (q == N);                 // a run completed exactly at N earlier
+  uint32_t mode = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  uint64_t cur = 0;
   while (ps.pos < hard) {
-    if (q == N && ps.g == 0 && (ps.dk == 0 || closed)) {
-      // every pixel is accounted for; the reference still reads one more prefix
-      // (code.rs:660): if it is a run digit the reference copies past its buffer
-      if (strict) {
-        uint64_t px = 0;
-        const uint32_t sym = parse_step(src, T, ps, px);
-        if (sym >= (uint32_t)P_RUN1) set_status(&a.status[f], NICE_E_FORMAT);
-      }
-      return;
-    }
-    if (ps.pos >= end) return;
-    const uint64_t at = ps.pos;
-    const uint32_t g0 = ps.g, dk0 = ps.dk;
-    const uint64_t acc0 = ps.acc;
-    uint64_t px = 0;
-    const uint32_t sym = parse_step(src, T, ps, px);
-    if (g0 != 0) continue;                 // payload symbol
-    if (sym >= (uint32_t)P_RUN1) {         // run digit
-      if (q == N && dk0 == 0) {            // digit right after the last pixel
-        if (strict) set_status(&a.status[f], NICE_E_FORMAT);
+    if (ps.g == 0) {
+      if (q == N && (ps.dk == 0 || closed)) {
+        // every pixel is accounted for; the reference still reads one more prefix
+        // (code.rs:660): a run digit there makes it copy past its buffer
+        if (strict) {
+          uint64_t px = 0;
+          const uint32_t sym = parse_step(src, T, ps, px);
+          if (sym >= (uint32_t)P_RUN1) set_status(&a.status[f], NICE_E_FORMAT);
+        }
         return;
       }
-      q += px;
-      if (q > N) { set_status(&a.status[f], NICE_E_FORMAT); return; }
-      if (q == N) {                         // the final run reaches the image end
-        put_run_bounds(a, fb, N - (ps.acc + 1), N, ps.pos);
-        closed = true;
+      if (ps.pos >= end) return;          // next chunk continues from here
+    }
+    const uint32_t g0 = ps.g, dk0 = ps.dk;
+    uint64_t px = 0;
+    const uint32_t sym = parse_step(src, T, ps, px);
+    if (g0 == 0) {
+      if (sym >= (uint32_t)P_RUN1) {      // run digit
+        if (q == N && dk0 == 0) {         // a digit right after the last pixel
+          if (strict) set_status(&a.status[f], NICE_E_FORMAT);
+          return;
+        }
+        q += px;
+        if (q > N) { set_status(&a.status[f], NICE_E_FORMAT); return; }
+        if (q == N) closed = true;
+        continue;
       }
+      closed = false;
+      mode = sym;
+      cur = q;
+      q += 1;
       continue;
     }
-    // a pixel prefix: closes the previous pixel's run
-    if (dk0 > 0 && !closed) put_run_bounds(a, fb, q - (acc0 + 1), q, at);
-    closed = false;
-    put_bound(a, fb, q, at, 0);
-    q += 1;
+    switch (g0) {
+      case 1: case 2: case 5: case 9: case 10: s0 = sym; break;
+      case 3: case 6: case 11: s1 = sym; break;
+      case 4: case 7: case 12: s2 = sym; break;
+      default: s3 = sym; break;
+    }
+    if (ps.g == 0) {                       // payload complete
+      uint32_t r;
+      const int e = make_record(a, cur, mode, s0, s1, s2, s3, &r);
+      if (e) { set_status(&a.status[f], e); return; }
+      rec[cur] = r;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // D5: reconstruction.
 // ---------------------------------------------------------------------------
-struct Ival {       // cyclic interval [lo, lo+len] mod 256; len 255 = unknown
-  uint32_t lo, len;
-};
-__device__ __forceinline__ Ival iv_exact(uint32_t v) { return Ival{v & 255u, 0u}; }
-__device__ __forceinline__ Ival iv_add(Ival a, uint32_t c) { return Ival{(a.lo + c) & 255u, a.len}; }
-__device__ __forceinline__ Ival iv_avg(Ival l, uint32_t u, uint32_t c) {
+// Per-channel cyclic interval [lo, lo+len] mod 256 packed as lo | len << 8;
+// len 255 = unknown.  A pixel is three of them.
+__device__ __forceinline__ uint32_t iv_add(uint32_t a, uint32_t c) {
+  return ((a + c) & 255u) | (a & 0xFF00u);
+}
+__device__ __forceinline__ uint32_t iv_avg(uint32_t l, uint32_t u, uint32_t c) {
+  const uint32_t llo = l & 255u, llen = l >> 8;
   uint32_t lo, hi;
-  if (l.lo + l.len <= 255u) { lo = (l.lo + u) >> 1; hi = (l.lo + l.len + u) >> 1; }
-  else { lo = u >> 1; hi = (255u + u) >> 1; }
-  return Ival{(lo + c) & 255u, hi - lo};
+  if (llo + llen <= 255u) { lo = (llo + u) >> 1; hi = (llo + llen + u) >> 1; }
+  else { lo = u >> 1; hi = (255u + u) >> 1; }   // wrapped interval: hull of both halves
+  return ((lo + c) & 255u) | ((hi - lo) << 8);
 }
-constexpr Ival IV_UNKNOWN = {0u, 255u};
+constexpr uint32_t IV_UNKNOWN = 255u << 8;
 
-struct Px3 { Ival c[3]; };
-
+struct Px3 { uint32_t c0, c1, c2; };
 __device__ __forceinline__ uint32_t pack_px(const Px3& p) {
-  return p.c[0].lo | (p.c[1].lo << 8) | (p.c[2].lo << 16);
+  return (p.c0 & 255u) | ((p.c1 & 255u) << 8) | ((p.c2 & 255u) << 16);
 }
-__device__ __forceinline__ bool px_exact(const Px3& p) {
-  return (p.c[0].len | p.c[1].len | p.c[2].len) == 0;
-}
+__device__ __forceinline__ bool px_exact(const Px3& p) { return ((p.c0 | p.c1 | p.c2) >> 8) == 0; }
 __device__ __forceinline__ Px3 px_from(uint32_t v) {
-  Px3 p;
-  p.c[0] = iv_exact(v & 255u); p.c[1] = iv_exact((v >> 8) & 255u); p.c[2] = iv_exact((v >> 16) & 255u);
-  return p;
+  return Px3{v & 255u, (v >> 8) & 255u, (v >> 16) & 255u};
 }
-__device__ __forceinline__ Px3 px_unknown() {
-  Px3 p; p.c[0] = IV_UNKNOWN; p.c[1] = IV_UNKNOWN; p.c[2] = IV_UNKNOWN; return p;
+__device__ __forceinline__ Px3 px_unknown() { return Px3{IV_UNKNOWN, IV_UNKNOWN, IV_UNKNOWN}; }
+__device__ __forceinline__ Px3 px_add(const Px3& r, uint32_t c) {
+  return Px3{iv_add(r.c0, c & 255u), iv_add(r.c1, (c >> 8) & 255u), iv_add(r.c2, (c >> 16) & 255u)};
+}
+__device__ __forceinline__ Px3 px_avg(const Px3& l, uint32_t U, uint32_t c) {
+  return Px3{iv_avg(l.c0, U & 255u, c & 255u), iv_avg(l.c1, (U >> 8) & 255u, (c >> 8) & 255u),
+             iv_avg(l.c2, (U >> 16) & 255u, (c >> 16) & 255u)};
 }
 
 struct RecLds {
-  DecTables T;
   uint32_t y4tail[4];
-  uint32_t fin;             // bitmask of final segments (<= 64 segments: lo/hi words)
-  uint32_t fin_hi;
+  int32_t ref_k[16], ref_d[16];
+  int64_t ref_off[16];
   int32_t err;
+  uint32_t pad[3];
 };
 
-// Resolve a reference at linear offset off = k*W + d from pixel (x, y).
-// Returns true with the packed value if it is known, false if unknown.
+// Row storage: R rows x W packed RGB (R = 4 for W >= 3, else 8), the current
+// row's known-bits, the last 3 pixels of row y-4 (offsets 3W+1, 3W+3).
 struct RowCtx {
-  uint32_t* ring;           // R rows x W (packed RGB), R = 4 for W >= 3 else 8
-  uint32_t* known;          // W bits for the current row
-  const uint32_t* y4tail;   // last 3 pixels of row y-4 at [W-3..W-1] -> [0..2]
-  uint32_t W, y, rmask;     // rmask = R - 1
-  bool same_row_ok;         // far same-row reads allowed (rows in LDS, or after a barrier)
+  uint32_t* ring;
+  uint32_t* known;
+  const uint32_t* y4tail;
+  uint32_t W, y, rmask;
+  bool same_row_ok;   // far same-row reads allowed (rows in LDS, or after a barrier)
   __device__ __forceinline__ uint32_t* row(uint32_t r) const { return ring + (size_t)(r & rmask) * W; }
 };
 
+// Pixel at offset off = k*W + d >= 4 before (x, y): 1 known, 0 unknown.
 __device__ __forceinline__ int ref_lookup(const RowCtx& rc, uint32_t x, int k, int d, uint32_t* v) {
-  // returns 1: value in *v; 0: unknown; -1: invalid (before the image)
   int64_t jx = (int64_t)x - d;
   int64_t jy = (int64_t)rc.y - k;
   while (jx < 0) { jx += rc.W; --jy; }
   while (jx >= (int64_t)rc.W) { jx -= rc.W; ++jy; }
-  if (jy < 0) return -1;
   if (jy == (int64_t)rc.y) {
     if (!rc.same_row_ok || !((rc.known[jx >> 5] >> (jx & 31)) & 1u)) return 0;
     *v = rc.row(rc.y)[jx];
     return 1;
   }
   if (jy >= (int64_t)rc.y - (int64_t)rc.rmask) { *v = rc.row((uint32_t)jy)[jx]; return 1; }
-  // row y-4 with R = 4: only the last 3 columns are reachable (offsets 3W+1, 3W+3)
   *v = rc.y4tail[jx - (rc.W - 3)];
   return 1;
 }
 
-// Decode one pixel (coded or run member) into intervals.  recent[0..2] hold
-// pixels i-1, i-2, i-3.  Returns 0 on success, negative error code.
-template <class Tab>
-__device__ __forceinline__ int rec_pixel(const BitSrc& src, const Tab& T, const RowCtx& rc, uint32_t x,
-                                         uint64_t& pos, uint64_t& run, const Px3 recent[3], Px3& out,
-                                         uint64_t N, uint64_t i) {
-  if (run > 0) {
-    out = recent[0];
-    --run;
-    return 0;
-  }
-  uint64_t p = pos;
-  const uint32_t mode = dec_symbol(src, T, S_PREFIX, &p);
+// Pixels [x0, x_stop) of the current row from their records; r0..r2 are the
+// pixels before x0 (intervals).  Exact results go to the row and `known`.
+// Returns the last segment-local index left unknown (-1: none).
+__device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, const uint32_t* recs,
+                                           uint32_t x0, uint32_t x_stop, Px3 r0, Px3 r1, Px3 r2) {
+  int last_unknown = -1;
   const uint32_t y = rc.y;
-  const bool has_up = y > 0;
-  uint32_t U = 0;
-  if (has_up) U = rc.row(y - 1)[x];
-  switch (mode) {
-    case P_BACK_REF: {
-      const uint32_t k = dec_symbol(src, T, S_BACK_REF, &p);
-      if (k >= 5) return NICE_E_FORMAT;
-      const int rk = br_rows((int)k), dk = br_px((int)k);
-      const int64_t off = (int64_t)rk * rc.W + dk;
-      if ((int64_t)i < off || off < 0) return NICE_E_FORMAT;   // code.rs:634 underflow
-      if (off == 0) { out = px_from(0u); break; }   // self copy of a fresh (zeroed) pixel
-      if (off <= 3) { out = recent[off - 1]; break; }
-      uint32_t v;
-      const int r = ref_lookup(rc, x, rk, dk, &v);
-      if (r < 0) return NICE_E_FORMAT;
-      out = r ? px_from(v) : px_unknown();
-      break;
-    }
-    case P_SMALL_DIFF: {
-      const uint32_t sd = dec_symbol(src, T, S_SMALL_DIFF, &p);
-      const int rd = (int)(sd % 7), t1 = (int)(sd / 7);
-      const int gd = t1 % 7, bd = t1 / 7;
-      const int dd[3] = {rd - 3, gd - 3, bd - 3};
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const uint32_t cc = (uint32_t)dd[c] & 255u;
-        out.c[c] = has_up ? iv_avg(recent[0].c[c], (U >> (8 * c)) & 255u, cc) : iv_add(recent[0].c[c], cc);
-      }
-      break;
-    }
-    case P_LUMA2: {
-      if (!has_up) return NICE_E_FORMAT;
-      const uint32_t gs = dec_symbol(src, T, S_LUMA2_BASE, &p);
-      const uint32_t rs = dec_symbol(src, T, S_LUMA2_R, &p);
-      const uint32_t bs = dec_symbol(src, T, S_LUMA2_B, &p);
-      const uint32_t g = (gs - 32u) & 255u;
-      const uint32_t cc[3] = {(rs - 16u + g) & 255u, g, (bs - 16u + g) & 255u};
-#pragma unroll
-      for (int c = 0; c < 3; ++c) out.c[c] = iv_avg(recent[0].c[c], (U >> (8 * c)) & 255u, cc[c]);
-      break;
-    }
-    case P_LUMA: {
-      const uint32_t k = dec_symbol(src, T, S_LUMA_REF, &p);
-      if (k >= 11) return NICE_E_FORMAT;
-      const uint32_t gs = dec_symbol(src, T, S_LUMA_BASE, &p);
-      const uint32_t rs = dec_symbol(src, T, S_LUMA_OTHER, &p);
-      const uint32_t bs = dec_symbol(src, T, S_LUMA_OTHER, &p);
-      const uint32_t g = (gs - 32u) & 255u;
-      const uint32_t cc[3] = {(rs - 16u + g) & 255u, g, (bs - 16u + g) & 255u};
-      const int rk = lr_rows((int)k), dk = lr_px((int)k);
-      const int64_t off = (int64_t)rk * rc.W + dk;
-      if ((int64_t)i < off || off < 0) return NICE_E_FORMAT;  // usize wrap/underflow, code.rs:548,624
-      Px3 ref;
-      if (off == 0) ref = px_from(0u);   // reads the not-yet-written pixel itself (zeroed)
-      else if (off <= 3) ref = recent[off - 1];
+  uint32_t* row = rc.row(y);
+  const uint32_t* up = y > 0 ? rc.row(y - 1) : nullptr;
+  for (uint32_t x = x0; x < x_stop; ++x) {
+    const uint32_t r = recs[x];
+    Px3 v;
+    if (r == REC_RUN) {
+      v = r0;
+    } else if (!(r & REC_REF)) {
+      v = y > 0 ? px_avg(r0, up[x], r) : px_add(r0, r);
+    } else {
+      const int id = (int)((r >> 24) & 15u);
+      const int64_t off = L.ref_off[id];
+      Px3 src;
+      if (off == 0) src = px_from(0u);       // the pixel itself, not yet written (zeroed)
+      else if (off == 1) src = r0;
+      else if (off == 2) src = r1;
+      else if (off == 3) src = r2;
       else {
-        uint32_t v;
-        const int r = ref_lookup(rc, x, rk, dk, &v);
-        if (r < 0) return NICE_E_FORMAT;
-        ref = r ? px_from(v) : px_unknown();
+        uint32_t u;
+        src = ref_lookup(rc, x, L.ref_k[id], L.ref_d[id], &u) ? px_from(u) : px_unknown();
       }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) out.c[c] = iv_add(ref.c[c], cc[c]);
-      break;
+      v = px_add(src, r);
     }
-    case P_RGB: {
-      const uint32_t r0 = dec_symbol(src, T, S_RGB, &p);
-      const uint32_t r1 = dec_symbol(src, T, S_RGB, &p);
-      const uint32_t r2 = dec_symbol(src, T, S_RGB, &p);
-      const uint32_t cc[3] = {r0, r1, r2};
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        out.c[c] = has_up ? iv_avg(recent[0].c[c], (U >> (8 * c)) & 255u, cc[c]) : iv_add(recent[0].c[c], cc[c]);
-      break;
+    if (px_exact(v)) {
+      row[x] = pack_px(v);
+      atomicOr(&rc.known[x >> 5], 1u << (x & 31));
+    } else {
+      last_unknown = (int)(x - x0);
     }
-    default:
-      return NICE_E_FORMAT;   // a run digit where a pixel must start
+    r2 = r1; r1 = r0; r0 = v;
   }
-  // run digits following the pixel (code.rs:660-671)
-  uint64_t acc = 0;
-  uint32_t dk = 0;
-  const uint64_t rem = N - i - 1;       // pixels after this one
-  if (rem > 0) {
-    while (true) {
-      uint64_t p2 = p;
-      const uint32_t nx = dec_symbol(src, T, S_PREFIX, &p2);
-      if (nx < (uint32_t)P_RUN1) break;
-      acc += (uint64_t)(nx - P_RUN1) << ((3u * dk) & 63u);
-      ++dk;
-      p = p2;
-      if (acc + 1 >= rem) break;        // the run reaches the image end
-      if (dk > 21) return NICE_E_FORMAT;
-    }
-    if (dk > 0) {
-      run = acc + 1;
-      if (run > rem) return NICE_E_FORMAT;
-    }
-  }
-  pos = p;
-  return 0;
+  return last_unknown;
 }
 
-__global__ __launch_bounds__(64) void dec_reconstruct(DecArgs a) {
+// The row ring lives in LDS when it fits (LDS_ROWS) -- the address space must
+// be static: a runtime LDS-or-global pointer compiles to flat_* accesses, and
+// every flat access waits for all outstanding global loads.
+template <bool LDS_ROWS>
+__device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   RecLds& L = *reinterpret_cast<RecLds*>(smem);
   const uint32_t W = a.W, H = a.H;
   const uint32_t R = W >= 3 ? 4u : 8u;
   const uint32_t kw = (W + 31) / 32;
-  uint32_t* known = reinterpret_cast<uint32_t*>(smem + ((sizeof(RecLds) + 15) & ~15ull));
-  uint32_t* ring = a.rows_in_lds ? known + ((kw + 3) & ~3u)
-                                 : a.rowbuf + (uint64_t)blockIdx.x * R * W;
+  static_assert(sizeof(RecLds) <= 512, "host LDS sizing assumes RecLds <= 512 B");
+  uint32_t* known = reinterpret_cast<uint32_t*>(smem + 512);
+  uint32_t* recbuf = known + ((kw + 3) & ~3u);            // W records of the current row
+  uint32_t* ring;
+  if constexpr (LDS_ROWS) ring = recbuf + ((W + 3) & ~3u);
+  else ring = a.rowbuf + (uint64_t)blockIdx.x * R * W;
   const uint32_t f = blockIdx.x;
   const int lane = threadIdx.x;
   if (a.status[f] != 0) return;
-  load_tables(L.T, reinterpret_cast<const DecTables*>(a.tables) + f);
+  if (lane < 16) {
+    L.ref_k[lane] = ref_rows(lane);
+    L.ref_d[lane] = ref_px_off(lane);
+    L.ref_off[lane] = (int64_t)ref_rows(lane) * W + ref_px_off(lane);
+  }
   if (lane == 0) L.err = 0;
   __syncthreads();
   const uint64_t N = (uint64_t)W * H;
   const uint32_t S = a.seg, nseg = a.nseg;
-  const uint64_t len = a.stream_len[f];
-  BitSrc src{a.streams + (uint64_t)f * a.stream_stride, len};
-  const SegBound* bounds = reinterpret_cast<const SegBound*>(a.bounds) + (uint64_t)f * H * nseg;
+  const uint32_t* recs = a.recs + (uint64_t)f * N;
   uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
   const uint32_t OC = a.out_channels;
   const uint8_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 255 : 0;
+  const bool active = (uint32_t)lane < nseg;
+  const uint32_t x0 = lane * S;
+  const uint32_t x1 = active ? min(x0 + S, W) : x0;
+  const uint32_t seglen = x1 - x0;
 
   for (uint32_t y = 0; y < H; ++y) {
-    RowCtx rc{ring, known, L.y4tail, W, y, R - 1, a.rows_in_lds != 0};
-    // save row y-4's tail before its ring slot is reused for row y
+    RowCtx rc{ring, known, L.y4tail, W, y, R - 1, LDS_ROWS};
     if (R == 4 && y >= 4 && lane < 3) L.y4tail[lane] = rc.row(y)[W - 3 + lane];
     for (uint32_t w = lane; w < kw; w += 64) known[w] = 0;
+    // this row's records, coalesced
+    const uint32_t* rrow = recs + (uint64_t)y * W;
+    for (uint32_t x = lane; x < W; x += 64) recbuf[x] = rrow[x];
     __syncthreads();
-
-    const bool active = (uint32_t)lane < nseg;
-    const uint32_t x0 = lane * S;
-    const uint32_t x1 = active ? min(x0 + S, W) : x0;
-    uint64_t pos0 = 0, run0 = 0;
-    if (active) { pos0 = bounds[(uint64_t)y * nseg + lane].pos; run0 = bounds[(uint64_t)y * nseg + lane].run; }
-    // exact pixel at linear index j < y*W + x0 (final rows / final left segments)
     auto linear_px = [&](int64_t j) -> uint32_t {
       if (j < 0) return 0u;   // pixel 0's left neighbour is itself, not yet written (0)
       const uint64_t jy = (uint64_t)j / W, jx = (uint64_t)j - jy * W;
       return (R == 4 && jy + 4 == y) ? L.y4tail[jx - (W - 3)] : rc.row((uint32_t)jy)[jx];
     };
-    Px3 recent[3];
+    Px3 r0, r1, r2;
     if (lane == 0) {
-      // entry = pixels i-1, i-2, i-3 before the row start, all final
-      for (int k = 0; k < 3; ++k) recent[k] = px_from(linear_px((int64_t)y * W - 1 - k));
+      r0 = px_from(linear_px((int64_t)y * W - 1));
+      r1 = px_from(linear_px((int64_t)y * W - 2));
+      r2 = px_from(linear_px((int64_t)y * W - 3));
     } else {
-      recent[0] = px_unknown(); recent[1] = px_unknown(); recent[2] = px_unknown();
+      r0 = px_unknown(); r1 = px_unknown(); r2 = px_unknown();
     }
-    // speculative pass (lane 0 is exact from the start)
+    // speculative pass: lane 0 starts exact, the others from an unknown entry
     int last_unknown = -1;
-    int err = 0;
-    if (active) {
-      uint64_t pos = pos0, run = run0;
-      for (uint32_t x = x0; x < x1; ++x) {
-        Px3 v;
-        const uint64_t i = (uint64_t)y * W + x;
-        err = rec_pixel(src, L.T, rc, x, pos, run, recent, v, N, i);
-        if (err) break;
-        if (px_exact(v)) {
-          rc.row(y)[x] = pack_px(v);
-          atomicOr(&known[x >> 5], 1u << (x & 31));
-        } else {
-          last_unknown = (int)(x - x0);
-        }
-        recent[2] = recent[1]; recent[1] = recent[0]; recent[0] = v;
-      }
-    }
-    if (err) atomicCAS(&L.err, 0, err);
-    // fix-up rounds: a segment is final once it has no unknown pixel
+    if (active) last_unknown = run_segment(rc, L, recbuf, x0, x1, r0, r1, r2);
+    // fix-up rounds: an unconverged segment is recomputed exactly as soon as the
+    // three pixels before it are exact (left segment converged before its last
+    // three pixels, or already fixed) -- normally all in one parallel round
     unsigned long long fin = __ballot(!active || last_unknown < 0);
+    unsigned long long tail_ok = __ballot(!active || last_unknown < 0 ||
+                                          (seglen >= 3 && last_unknown < (int)seglen - 3));
+    if (a.stats && lane == 0) {
+      atomicAdd(&a.stats[0], 1ull);
+      atomicAdd(&a.stats[1], (unsigned long long)__popcll(~fin));
+      atomicAdd(&a.stats[2], (unsigned long long)__popcll(~tail_ok));
+    }
+    if (a.stats && active && last_unknown >= 0) atomicAdd(&a.stats[3], (unsigned long long)(last_unknown + 1));
     __syncthreads();
     rc.same_row_ok = true;
-    while (fin != ~0ull && L.err == 0) {
+    while (fin != ~0ull) {
       const bool mine = !((fin >> lane) & 1ull);
-      const bool left_ok = lane == 0 || ((fin >> (lane - 1)) & 1ull);
+      const bool left_ok = lane == 0 || (((fin | tail_ok) >> (lane - 1)) & 1ull);
       const bool ready = mine && left_ok;
       if (ready) {
-        for (int k = 0; k < 3; ++k) recent[k] = px_from(linear_px((int64_t)y * W + x0 - 1 - k));
-        uint64_t pos = pos0, run = run0;
-        for (uint32_t jx = 0; jx <= (uint32_t)last_unknown; ++jx) {
-          const uint32_t x = x0 + jx;
-          Px3 v;
-          const uint64_t i = (uint64_t)y * W + x;
-          err = rec_pixel(src, L.T, rc, x, pos, run, recent, v, N, i);
-          if (err) break;
-          if (!px_exact(v)) { err = NICE_E_FORMAT; break; }   // exact inputs give exact outputs
-          rc.row(y)[x] = pack_px(v);
-          atomicOr(&known[x >> 5], 1u << (x & 31));
-          recent[2] = recent[1]; recent[1] = recent[0]; recent[0] = v;
-        }
-        if (err) atomicCAS(&L.err, 0, err);
+        r0 = px_from(linear_px((int64_t)y * W + x0 - 1));
+        r1 = px_from(linear_px((int64_t)y * W + x0 - 2));
+        r2 = px_from(linear_px((int64_t)y * W + x0 - 3));
+        const int lu = run_segment(rc, L, recbuf, x0, x0 + (uint32_t)last_unknown + 1, r0, r1, r2);
+        if (lu >= 0) atomicCAS(&L.err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         last_unknown = -1;
       }
       __syncthreads();
       fin |= __ballot(ready);
+      tail_ok |= fin;
+      if (a.stats && lane == 0) atomicAdd(&a.stats[4], 1ull);
     }
     __syncthreads();
     if (L.err) break;
     // emit the row in the caller's pixel format
     uint8_t* orow = outp + (uint64_t)y * W * OC;
-    for (uint32_t x = lane; x < W; x += 64) {
-      const uint32_t v = rc.row(y)[x];
-      uint8_t* o = orow + (uint64_t)x * OC;
-      o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16);
-      if (OC == 4) o[3] = alpha;
+    const uint32_t* row = rc.row(y);
+    if (OC == 4) {
+      uint32_t* o32 = reinterpret_cast<uint32_t*>(orow);
+      for (uint32_t x = lane; x < W; x += 64) o32[x] = row[x] | ((uint32_t)alpha << 24);
+    } else {
+      for (uint32_t x = lane; x < W; x += 64) {
+        const uint32_t v = row[x];
+        uint8_t* o = orow + (uint64_t)x * 3;
+        o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16);
+      }
     }
     __syncthreads();
   }
   if (lane == 0 && L.err) set_status(&a.status[f], L.err);
+}
+
+__global__ __launch_bounds__(64) void dec_reconstruct(DecArgs a) {
+  if (a.rows_in_lds) dec_reconstruct_body<true>(a);
+  else dec_reconstruct_body<false>(a);
 }
 
 }  // namespace nice

@@ -160,7 +160,9 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
         WinAcc acc{&tw, p + 3};
         if (fast) classify<true>((uint32_t)(start + p), a.W, acc, s);
         else classify<false>((uint32_t)(start + p), a.W, acc, s);
-        for (uint32_t k = 0; k < s.n; ++k) atomicAdd(&hist[s.b[k]], 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((uint32_t)k < s.n) atomicAdd(&hist[s.b[k]], 1u);
         const int nx = next_coded_local(mask, p);
         if (nx < count) {
           const uint64_t run = (uint64_t)(nx - p - 1);
@@ -545,7 +547,9 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
       if (fast) classify<true>((uint32_t)(start + p), a.W, acc, sy[r]);
       else classify<false>((uint32_t)(start + p), a.W, acc, sy[r]);
       uint32_t n = tbl[BIN_PREFIX + sy[r].mode] & 31u;
-      for (uint32_t k = 0; k < sy[r].n; ++k) n += tbl[sy[r].b[k]] & 31u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((uint32_t)k < sy[r].n) n += tbl[sy[r].b[k]] & 31u;
       const int nx = next_coded_local(mask, p);
       const uint64_t nxt = (nx < count) ? (uint64_t)(start + nx) : (uint64_t)next_tile_px;
       const uint64_t run = nxt - (uint64_t)(start + p) - 1;
@@ -597,10 +601,13 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
     uint32_t e = tbl[BIN_PREFIX + sy[r].mode];
     or_bits(bits, pos, e >> 5, e & 31u);
     pos += e & 31u;
-    for (uint32_t k = 0; k < sy[r].n; ++k) {
-      e = tbl[sy[r].b[k]];
-      or_bits(bits, pos, e >> 5, e & 31u);
-      pos += e & 31u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if ((uint32_t)k < sy[r].n) {
+        e = tbl[sy[r].b[k]];
+        or_bits(bits, pos, e >> 5, e & 31u);
+        pos += e & 31u;
+      }
     }
     if (runs[r] > 0) {
       uint64_t m = runs[r] - 1;
@@ -752,7 +759,9 @@ __global__ __launch_bounds__(64) void enc_serial(EncArgs a) {
     GlobalAcc acc{frame, (int)a.C, a.W, (int64_t)i};
     classify<false>((uint32_t)i, a.W, acc, s);
     emit(BIN_PREFIX + s.mode);
-    for (uint32_t k = 0; k < s.n; ++k) emit(s.b[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((uint32_t)k < s.n) emit(s.b[k]);
     const uint32_t X = acc(0, 0);
     uint64_t j = i + 1;
     while (j < N && load_spread(frame, (int64_t)j, a.C) == X) ++j;

@@ -73,10 +73,11 @@ struct DecArgs {
   uint32_t max_chunks, chunk_blocks;  // per frame
   unsigned long long* chunk_px;       // n_frames * max_chunks
   unsigned long long* chunk_start;    // n_frames * max_chunks
-  void* bounds;                       // n_frames * H * nseg SegBound
+  uint32_t* recs;                     // n_frames * W * H per-pixel records
   uint32_t seg, nseg;
   uint32_t rows_in_lds;               // 1: row ring in LDS, 0: in rowbuf
   uint32_t* rowbuf;                   // n_frames * R * W (when not in LDS)
+  unsigned long long* stats;          // optional diagnostics (NICE_DEC_STATS=1), else null
 };
 
 struct ParseState;
@@ -85,7 +86,7 @@ __global__ void dec_init_entries(DecArgs a, ParseState* e);
 __global__ void dec_sync(DecArgs a, const ParseState* in, ParseState* out, uint32_t* changed);
 __global__ void dec_count(DecArgs a, const ParseState* entry);
 __global__ void dec_scan(DecArgs a);
-__global__ void dec_bounds(DecArgs a, const ParseState* entry);
+__global__ void dec_emit(DecArgs a, const ParseState* entry);
 __global__ void dec_reconstruct(DecArgs a);
 
 }  // namespace nice

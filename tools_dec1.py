@@ -1,0 +1,11 @@
+"""Diagnostic: decode one 4K RGBA SYN-v1 stream through the product path."""
+import importlib, os, sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+nice = importlib.import_module("fast-losless-image-compression-format_amd")
+from oracle import oracle as O
+w, h = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))
+px = O.gen_syn_v1(w, h, 4, 1)
+s = O.encode(px, w, h, 4)
+d, _ = nice.decode_bytes(s)
+print("ok", np.array_equal(np.frombuffer(d, np.uint8).reshape(-1, 4)[:, :3], px.reshape(-1, 4)[:, :3]))
