@@ -320,7 +320,7 @@ RecGeom rec_geom(uint32_t w) {
   g.nseg = w ? (w + s - 1) / s : 1;
   g.R = w >= 3 ? 4 : 8;
   const size_t kw = (w + 31) / 32;
-  const size_t head = 512 + align_up(kw, 4) * 4 + align_up(w, 4) * 4;   // RecLds <= 512 B
+  const size_t head = 512 + align_up(kw, 4) * 4 + align_up(w, 4) * 4;   // RecLds <= 512 B, records
   const size_t ring = (size_t)g.R * w * 4;
   g.in_lds = head + ring <= 150 * 1024;
   g.lds = g.in_lds ? head + ring : head;
@@ -461,9 +461,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
     ea = eb;
     eb = t;
   }
-  tm.begin(NICE_PH_DEC_COUNT, st);
-  hipLaunchKernelGGL(dec_count, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
-  tm.end(st);
+  // the last sync iteration (no entry changed) already produced chunk_px
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
@@ -476,21 +474,22 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
   static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
   unsigned long long* dstats = nullptr;
-  if (want_stats && hipMalloc(&dstats, 64) == hipSuccess) {
-    (void)hipMemsetAsync(dstats, 0, 64, st);
+  if (want_stats && hipMalloc(&dstats, 128) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 128, st);
     a.stats = dstats;
   }
   tm.begin(NICE_PH_DEC_RECON, st);
   hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
   tm.end(st);
   if (dstats) {
-    unsigned long long h[8] = {0};
-    (void)hipMemcpyAsync(h, dstats, 64, hipMemcpyDeviceToHost, st);
+    unsigned long long h[16] = {0};
+    (void)hipMemcpyAsync(h, dstats, 128, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
             "[nice dec stats] rows=%llu unconverged_segs=%llu tail_unknown_segs=%llu "
-            "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u\n",
-            h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg);
+            "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
+            "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
+            h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
     (void)hipFree(dstats);
   }
   NICE_HIP(hipGetLastError());

@@ -187,11 +187,10 @@ __device__ inline void load_tables(DecTables& dst, const DecTables* src) {
 // contribution; returns the symbol.  Run digits contribute d << 3k (+1 for the
 // first digit), so per-chunk pixel counts are additive.
 template <class Tab>
-__device__ __forceinline__ uint32_t parse_step(const BitSrc& src, const Tab& T, ParseState& ps,
+__device__ __forceinline__ uint32_t parse_step(LaneBits& br, const Tab& T, ParseState& ps,
                                                uint64_t& px) {
-  uint64_t pos = ps.pos;
-  const uint32_t sym = dec_symbol(src, T, gs_stream((int)ps.g), &pos);
-  ps.pos = pos;
+  const uint32_t sym = lane_symbol(br, T, gs_stream((int)ps.g));
+  ps.pos = br.pos;
   if (ps.g == 0) {
     if (sym >= (uint32_t)P_RUN1) {
       const uint32_t d = sym - P_RUN1;
@@ -252,14 +251,20 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, const ParseState* in,
   __syncthreads();
   const uint32_t j = jb * 256u + threadIdx.x;
   if (j >= nc) return;
-  BitSrc src{a.streams + (uint64_t)f * a.stream_stride, len};
   const uint64_t base = (uint64_t)f * a.max_chunks;
   ParseState ps = in[base + j];
   if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
+  LaneBits br;
+  br.p = a.streams + (uint64_t)f * a.stream_stride;
+  br.len = len;
+  br.seek(ps.pos);
   const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
   const uint64_t hard = len * 8 + 64;
+  const uint64_t N = (uint64_t)a.W * a.H;
   uint64_t px = 0;
-  while (ps.pos < end && ps.pos < hard) parse_step(src, T, ps, px);
+  while (ps.pos < end && ps.pos < hard && px <= N) parse_step(br, T, ps, px);
+  // pixels this chunk produces from its current entry: exact once entries are final
+  a.chunk_px[base + j] = px;
   if (j + 1 < nc) {
     const ParseState old = in[base + j + 1];
     out[base + j + 1] = ps;
@@ -284,15 +289,18 @@ __global__ __launch_bounds__(256) void dec_count(DecArgs a, const ParseState* en
   __syncthreads();
   const uint32_t j = jb * 256u + threadIdx.x;
   if (j >= nc) return;
-  BitSrc src{a.streams + (uint64_t)f * a.stream_stride, len};
   const uint64_t base = (uint64_t)f * a.max_chunks;
   ParseState ps = entry[base + j];
   if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
+  LaneBits br;
+  br.p = a.streams + (uint64_t)f * a.stream_stride;
+  br.len = len;
+  br.seek(ps.pos);
   const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
   const uint64_t hard = len * 8 + 64;
   uint64_t px = 0;
   const uint64_t N = (uint64_t)a.W * a.H;
-  while (ps.pos < end && ps.pos < hard && px <= N) parse_step(src, T, ps, px);
+  while (ps.pos < end && ps.pos < hard && px <= N) parse_step(br, T, ps, px);
   a.chunk_px[base + j] = px;
 }
 
@@ -407,9 +415,12 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a, const ParseState* ent
   const uint64_t N = (uint64_t)a.W * a.H;
   uint64_t q = a.chunk_start[base + j];   // pixels accounted before this chunk
   if (q > N) return;                      // past the image: tail bytes
-  BitSrc src{a.streams + (uint64_t)f * a.stream_stride, len};
   ParseState ps = entry[base + j];
   if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
+  LaneBits src;
+  src.p = a.streams + (uint64_t)f * a.stream_stride;
+  src.len = len;
+  src.seek(ps.pos);
   const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
   const uint64_t hard = len * 8 + 64;
   uint32_t* rec = a.recs + (uint64_t)f * N;
@@ -507,28 +518,39 @@ struct RecLds {
   int32_t ref_k[16], ref_d[16];
   int64_t ref_off[16];
   int32_t err;
-  uint32_t pad[3];
+  uint32_t first3;    // which of pixels 0..2 of the current row are written
+  uint32_t pad[2];
 };
 
-// Row storage: R rows x W packed RGB (R = 4 for W >= 3, else 8), the current
-// row's known-bits, the last 3 pixels of row y-4 (offsets 3W+1, 3W+3).
+// Exact packed-RGB arithmetic (R | G<<8 | B<<16), per byte mod 256.
+__device__ __forceinline__ uint32_t avg_rgb(uint32_t a, uint32_t b) {
+  return (a & b) + (((a ^ b) >> 1) & 0x7F7F7Fu);          // floor((a+b)/2) per byte
+}
+__device__ __forceinline__ uint32_t add_rgb(uint32_t a, uint32_t c) {
+  return (((a & 0x7F7F7Fu) + (c & 0x7F7F7Fu)) ^ ((a ^ c) & 0x808080u)) & 0xFFFFFFu;
+}
+
+// Row storage: R rows x W packed RGB (R = 4 for W >= 3, else 8) and the last 3
+// pixels of row y-4 (offsets 3W+1, 3W+3).
 struct RowCtx {
   uint32_t* ring;
-  uint32_t* known;
   const uint32_t* y4tail;
-  uint32_t W, y, rmask;
-  bool same_row_ok;   // far same-row reads allowed (rows in LDS, or after a barrier)
+  const uint32_t* first3;
+  uint32_t W, y, rmask, x0;
+  bool spec;          // speculative pass: other segments of this row may be unwritten
   __device__ __forceinline__ uint32_t* row(uint32_t r) const { return ring + (size_t)(r & rmask) * W; }
 };
 
 // Pixel at offset off = k*W + d >= 4 before (x, y): 1 known, 0 unknown.
+// Same-row targets are pixels 0..2 (offsets W-1, W-3 from the last columns) or,
+// with a single segment, this lane's own earlier pixels.
 __device__ __forceinline__ int ref_lookup(const RowCtx& rc, uint32_t x, int k, int d, uint32_t* v) {
   int64_t jx = (int64_t)x - d;
   int64_t jy = (int64_t)rc.y - k;
   while (jx < 0) { jx += rc.W; --jy; }
   while (jx >= (int64_t)rc.W) { jx -= rc.W; ++jy; }
   if (jy == (int64_t)rc.y) {
-    if (!rc.same_row_ok || !((rc.known[jx >> 5] >> (jx & 31)) & 1u)) return 0;
+    if (rc.spec && jx < (int64_t)rc.x0 && !(jx < 3 && ((*rc.first3 >> jx) & 1u))) return 0;
     *v = rc.row(rc.y)[jx];
     return 1;
   }
@@ -538,15 +560,21 @@ __device__ __forceinline__ int ref_lookup(const RowCtx& rc, uint32_t x, int k, i
 }
 
 // Pixels [x0, x_stop) of the current row from their records; r0..r2 are the
-// pixels before x0 (intervals).  Exact results go to the row and `known`.
-// Returns the last segment-local index left unknown (-1: none).
-__device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, const uint32_t* recs,
-                                           uint32_t x0, uint32_t x_stop, Px3 r0, Px3 r1, Px3 r2) {
+// pixels before x0 as intervals.  While any of the last three pixels is not
+// exact, cyclic-interval arithmetic tracks the possible values; once they all
+// collapse the rest of the segment runs on exact packed-RGB arithmetic.
+// Exact results go to the row.  Returns the last segment-local index left
+// unknown (-1: none).
+__device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, uint32_t* first3,
+                                           const uint32_t* recs, uint32_t x0, uint32_t x_stop,
+                                           Px3 r0, Px3 r1, Px3 r2) {
   int last_unknown = -1;
   const uint32_t y = rc.y;
   uint32_t* row = rc.row(y);
   const uint32_t* up = y > 0 ? rc.row(y - 1) : nullptr;
-  for (uint32_t x = x0; x < x_stop; ++x) {
+  uint32_t x = x0;
+  // ---- interval phase
+  while (x < x_stop && !(px_exact(r0) && px_exact(r1) && px_exact(r2))) {
     const uint32_t r = recs[x];
     Px3 v;
     if (r == REC_RUN) {
@@ -567,13 +595,39 @@ __device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, co
       }
       v = px_add(src, r);
     }
-    if (px_exact(v)) {
-      row[x] = pack_px(v);
-      atomicOr(&rc.known[x >> 5], 1u << (x & 31));
-    } else {
-      last_unknown = (int)(x - x0);
-    }
+    if (px_exact(v)) row[x] = pack_px(v);
+    else last_unknown = (int)(x - x0);
     r2 = r1; r1 = r0; r0 = v;
+    ++x;
+  }
+  // ---- exact phase
+  uint32_t p1 = pack_px(r0), p2 = pack_px(r1), p3 = pack_px(r2);
+  for (; x < x_stop; ++x) {
+    const uint32_t r = recs[x];
+    uint32_t v;
+    if (r == REC_RUN) {
+      v = p1;
+    } else if (!(r & REC_REF)) {
+      v = add_rgb(y > 0 ? avg_rgb(p1, up[x]) : p1, r);
+    } else {
+      const int id = (int)((r >> 24) & 15u);
+      const int64_t off = L.ref_off[id];
+      uint32_t src;
+      if (off == 0) src = 0u;
+      else if (off == 1) src = p1;
+      else if (off == 2) src = p2;
+      else if (off == 3) src = p3;
+      else if (!ref_lookup(rc, x, L.ref_k[id], L.ref_d[id], &src)) {
+        // a same-row pixel another lane has not written yet: leave the rest of
+        // the segment to the exact fix-up pass
+        last_unknown = (int)(x_stop - 1 - x0);
+        break;
+      }
+      v = add_rgb(src, r);
+    }
+    row[x] = v;
+    if (x < 3) atomicOr(first3, 1u << x);
+    p3 = p2; p2 = p1; p1 = v;
   }
   return last_unknown;
 }
@@ -589,8 +643,7 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   const uint32_t R = W >= 3 ? 4u : 8u;
   const uint32_t kw = (W + 31) / 32;
   static_assert(sizeof(RecLds) <= 512, "host LDS sizing assumes RecLds <= 512 B");
-  uint32_t* known = reinterpret_cast<uint32_t*>(smem + 512);
-  uint32_t* recbuf = known + ((kw + 3) & ~3u);            // W records of the current row
+  uint32_t* recbuf = reinterpret_cast<uint32_t*>(smem + 512) + ((kw + 3) & ~3u);   // row records
   uint32_t* ring;
   if constexpr (LDS_ROWS) ring = recbuf + ((W + 3) & ~3u);
   else ring = a.rowbuf + (uint64_t)blockIdx.x * R * W;
@@ -615,10 +668,12 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   const uint32_t x1 = active ? min(x0 + S, W) : x0;
   const uint32_t seglen = x1 - x0;
 
+  unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0;
   for (uint32_t y = 0; y < H; ++y) {
-    RowCtx rc{ring, known, L.y4tail, W, y, R - 1, LDS_ROWS};
+    const unsigned long long c0 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    RowCtx rc{ring, L.y4tail, &L.first3, W, y, R - 1, x0, true};
     if (R == 4 && y >= 4 && lane < 3) L.y4tail[lane] = rc.row(y)[W - 3 + lane];
-    for (uint32_t w = lane; w < kw; w += 64) known[w] = 0;
+    if (lane == 0) L.first3 = 0;
     // this row's records, coalesced
     const uint32_t* rrow = recs + (uint64_t)y * W;
     for (uint32_t x = lane; x < W; x += 64) recbuf[x] = rrow[x];
@@ -636,9 +691,10 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
     } else {
       r0 = px_unknown(); r1 = px_unknown(); r2 = px_unknown();
     }
+    const unsigned long long c1 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // speculative pass: lane 0 starts exact, the others from an unknown entry
     int last_unknown = -1;
-    if (active) last_unknown = run_segment(rc, L, recbuf, x0, x1, r0, r1, r2);
+    if (active) last_unknown = run_segment(rc, L, &L.first3, recbuf, x0, x1, r0, r1, r2);
     // fix-up rounds: an unconverged segment is recomputed exactly as soon as the
     // three pixels before it are exact (left segment converged before its last
     // three pixels, or already fixed) -- normally all in one parallel round
@@ -652,7 +708,8 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
     }
     if (a.stats && active && last_unknown >= 0) atomicAdd(&a.stats[3], (unsigned long long)(last_unknown + 1));
     __syncthreads();
-    rc.same_row_ok = true;
+    const unsigned long long c2 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    rc.spec = false;
     while (fin != ~0ull) {
       const bool mine = !((fin >> lane) & 1ull);
       const bool left_ok = lane == 0 || (((fin | tail_ok) >> (lane - 1)) & 1ull);
@@ -661,7 +718,8 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
         r0 = px_from(linear_px((int64_t)y * W + x0 - 1));
         r1 = px_from(linear_px((int64_t)y * W + x0 - 2));
         r2 = px_from(linear_px((int64_t)y * W + x0 - 3));
-        const int lu = run_segment(rc, L, recbuf, x0, x0 + (uint32_t)last_unknown + 1, r0, r1, r2);
+        const int lu = run_segment(rc, L, &L.first3, recbuf, x0, x0 + (uint32_t)last_unknown + 1,
+                                   r0, r1, r2);
         if (lu >= 0) atomicCAS(&L.err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         last_unknown = -1;
       }
@@ -671,6 +729,7 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
       if (a.stats && lane == 0) atomicAdd(&a.stats[4], 1ull);
     }
     __syncthreads();
+    const unsigned long long c3 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     if (L.err) break;
     // emit the row in the caller's pixel format
     uint8_t* orow = outp + (uint64_t)y * W * OC;
@@ -686,6 +745,14 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
       }
     }
     __syncthreads();
+    if (a.stats) {
+      const unsigned long long c4 = __builtin_amdgcn_s_memtime();
+      t_a += c1 - c0; t_b += c2 - c1; t_c += c3 - c2; t_d += c4 - c3;
+    }
+  }
+  if (a.stats && lane == 0) {
+    atomicAdd(&a.stats[5], t_a); atomicAdd(&a.stats[6], t_b);
+    atomicAdd(&a.stats[7], t_c); atomicAdd(&a.stats[8], t_d);
   }
   if (lane == 0 && L.err) set_status(&a.status[f], L.err);
 }
