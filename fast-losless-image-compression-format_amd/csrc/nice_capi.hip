@@ -274,7 +274,9 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   ctx->timer.end(st);
   if (T > 0) {
     ctx->timer.begin(NICE_PH_ENC_PACK, st);
-    hipLaunchKernelGGL(enc_pack, dim3((uint32_t)total_tiles), dim3(256), 0, st, a);
+    // persistent blocks in ticket order; <= 4 resident per CU (LDS ~37 KB each)
+    const uint64_t pblocks = total_tiles < 1024 ? total_tiles : 1024;
+    hipLaunchKernelGGL(enc_pack, dim3((uint32_t)pblocks), dim3(256), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_SERIAL, st);
     hipLaunchKernelGGL(enc_serial, dim3(n_frames), dim3(64), 0, st, a);
@@ -318,6 +320,9 @@ RecGeom rec_geom(uint32_t w) {
   if (s < 6) s = 6;
   g.seg = s;
   g.nseg = w ? (w + s - 1) / s : 1;
+  // the last segment (which runs to W) must be >= 6 pixels: its last three
+  // columns read pixels 0..2 of the same row, written by lane 0 at steps 0..2
+  if (g.nseg > 1 && w - (g.nseg - 1) * s < 6) g.nseg -= 1;
   g.R = w >= 3 ? 4 : 8;
   const size_t kw = (w + 31) / 32;
   const size_t head = 512 + align_up(kw, 4) * 4 + align_up(w, 4) * 4;   // RecLds <= 512 B, records

@@ -482,152 +482,105 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a, const ParseState* ent
 // ---------------------------------------------------------------------------
 // D5: reconstruction.
 // ---------------------------------------------------------------------------
-// Per-channel cyclic interval [lo, lo+len] mod 256 packed as lo | len << 8;
-// len 255 = unknown.  A pixel is three of them.
-__device__ __forceinline__ uint32_t iv_add(uint32_t a, uint32_t c) {
-  return ((a + c) & 255u) | (a & 0xFF00u);
-}
-__device__ __forceinline__ uint32_t iv_avg(uint32_t l, uint32_t u, uint32_t c) {
-  const uint32_t llo = l & 255u, llen = l >> 8;
-  uint32_t lo, hi;
-  if (llo + llen <= 255u) { lo = (llo + u) >> 1; hi = (llo + llen + u) >> 1; }
-  else { lo = u >> 1; hi = (255u + u) >> 1; }   // wrapped interval: hull of both halves
-  return ((lo + c) & 255u) | ((hi - lo) << 8);
-}
-constexpr uint32_t IV_UNKNOWN = 255u << 8;
-
-struct Px3 { uint32_t c0, c1, c2; };
-__device__ __forceinline__ uint32_t pack_px(const Px3& p) {
-  return (p.c0 & 255u) | ((p.c1 & 255u) << 8) | ((p.c2 & 255u) << 16);
-}
-__device__ __forceinline__ bool px_exact(const Px3& p) { return ((p.c0 | p.c1 | p.c2) >> 8) == 0; }
-__device__ __forceinline__ Px3 px_from(uint32_t v) {
-  return Px3{v & 255u, (v >> 8) & 255u, (v >> 16) & 255u};
-}
-__device__ __forceinline__ Px3 px_unknown() { return Px3{IV_UNKNOWN, IV_UNKNOWN, IV_UNKNOWN}; }
-__device__ __forceinline__ Px3 px_add(const Px3& r, uint32_t c) {
-  return Px3{iv_add(r.c0, c & 255u), iv_add(r.c1, (c >> 8) & 255u), iv_add(r.c2, (c >> 16) & 255u)};
-}
-__device__ __forceinline__ Px3 px_avg(const Px3& l, uint32_t U, uint32_t c) {
-  return Px3{iv_avg(l.c0, U & 255u, c & 255u), iv_avg(l.c1, (U >> 8) & 255u, (c >> 8) & 255u),
-             iv_avg(l.c2, (U >> 16) & 255u, (c >> 16) & 255u)};
-}
-
 struct RecLds {
   uint32_t y4tail[4];
   int32_t ref_k[16], ref_d[16];
-  int64_t ref_off[16];
+  int32_t ref_off32[16];   // k*W + d, clamped to [0, 4] (only 0..3 are special)
   int32_t err;
-  uint32_t first3;    // which of pixels 0..2 of the current row are written
-  uint32_t pad[2];
+  uint32_t pad[3];
 };
 
-// Exact packed-RGB arithmetic (R | G<<8 | B<<16), per byte mod 256.
-__device__ __forceinline__ uint32_t avg_rgb(uint32_t a, uint32_t b) {
-  return (a & b) + (((a ^ b) >> 1) & 0x7F7F7Fu);          // floor((a+b)/2) per byte
+// Per-channel cyclic intervals [lo, lo+len] (mod 256) for the three channels
+// in the "spread" layout (fields at bits 0, 10, 20 with two guard bits), so one
+// 32-bit op acts on all channels.  An exact value is an interval with len 0;
+// unknown is lo 0, len 255.  Rows are stored spread as well.
+constexpr uint32_t SP_K = 0xFFu | (0xFFu << 10) | (0xFFu << 20);
+constexpr uint32_t SP_K9 = 0x1FFu | (0x1FFu << 10) | (0x1FFu << 20);
+constexpr uint32_t SP_1 = 1u | (1u << 10) | (1u << 20);
+struct IvS { uint32_t lo, len; };
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {   // R | G<<8 | B<<16 -> spread
+  return (v & 0xFFu) | ((v & 0xFF00u) << 2) | ((v & 0xFF0000u) << 4);
 }
-__device__ __forceinline__ uint32_t add_rgb(uint32_t a, uint32_t c) {
-  return (((a & 0x7F7F7Fu) + (c & 0x7F7F7Fu)) ^ ((a ^ c) & 0x808080u)) & 0xFFFFFFu;
+__device__ __forceinline__ uint32_t unspread3(uint32_t v) {
+  return (v & 0xFFu) | ((v >> 2) & 0xFF00u) | ((v >> 4) & 0xFF0000u);
+}
+__device__ __forceinline__ IvS ivs_exact(uint32_t sp) { return IvS{sp, 0u}; }
+__device__ __forceinline__ IvS ivs_add(IvS a, uint32_t c) { return IvS{(a.lo + c) & SP_K, a.len}; }
+// floor((L + U) / 2) + c over an interval L: halves it unless it wraps past
+// 255, in which case the hull of both halves is [U/2, (255+U)/2].
+__device__ __forceinline__ IvS ivs_avg(IvS l, uint32_t u, uint32_t c) {
+  const uint32_t s = l.lo + l.len;
+  const uint32_t wm = ((s >> 8) & SP_1) * 0x3FFu;        // fields whose interval wraps
+  uint32_t lo1 = ((l.lo + u) >> 1) & SP_K;
+  uint32_t hi1 = ((s + u) >> 1) & SP_K9;
+  const uint32_t ulo = (u >> 1) & SP_K;
+  const uint32_t uhi = ((u + SP_K) >> 1) & SP_K9;
+  lo1 = (lo1 & ~wm) | (ulo & wm);
+  hi1 = (hi1 & ~wm) | (uhi & wm);
+  return IvS{(lo1 + c) & SP_K, hi1 - lo1};
 }
 
-// Row storage: R rows x W packed RGB (R = 4 for W >= 3, else 8) and the last 3
-// pixels of row y-4 (offsets 3W+1, 3W+3).
+// Row storage: R rows x W spread pixels (R = 4 for W >= 3, else 8) and the last
+// 3 pixels of row y-4 (offsets 3W+1, 3W+3).
 struct RowCtx {
   uint32_t* ring;
   const uint32_t* y4tail;
-  const uint32_t* first3;
-  uint32_t W, y, rmask, x0;
-  bool spec;          // speculative pass: other segments of this row may be unwritten
+  uint32_t W, y, rmask;
   __device__ __forceinline__ uint32_t* row(uint32_t r) const { return ring + (size_t)(r & rmask) * W; }
 };
 
-// Pixel at offset off = k*W + d >= 4 before (x, y): 1 known, 0 unknown.
-// Same-row targets are pixels 0..2 (offsets W-1, W-3 from the last columns) or,
-// with a single segment, this lane's own earlier pixels.
-__device__ __forceinline__ int ref_lookup(const RowCtx& rc, uint32_t x, int k, int d, uint32_t* v) {
-  int64_t jx = (int64_t)x - d;
-  int64_t jy = (int64_t)rc.y - k;
-  while (jx < 0) { jx += rc.W; --jy; }
-  while (jx >= (int64_t)rc.W) { jx -= rc.W; ++jy; }
-  if (jy == (int64_t)rc.y) {
-    if (rc.spec && jx < (int64_t)rc.x0 && !(jx < 3 && ((*rc.first3 >> jx) & 1u))) return 0;
-    *v = rc.row(rc.y)[jx];
-    return 1;
-  }
-  if (jy >= (int64_t)rc.y - (int64_t)rc.rmask) { *v = rc.row((uint32_t)jy)[jx]; return 1; }
-  *v = rc.y4tail[jx - (rc.W - 3)];
-  return 1;
-}
-
 // Pixels [x0, x_stop) of the current row from their records; r0..r2 are the
-// pixels before x0 as intervals.  While any of the last three pixels is not
-// exact, cyclic-interval arithmetic tracks the possible values; once they all
-// collapse the rest of the segment runs on exact packed-RGB arithmetic.
-// Exact results go to the row.  Returns the last segment-local index left
-// unknown (-1: none).
-__device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, uint32_t* first3,
-                                           const uint32_t* recs, uint32_t x0, uint32_t x_stop,
-                                           Px3 r0, Px3 r1, Px3 r2) {
+// pixels before x0 (intervals).  Branch-free step: the averaging value and the
+// reference value are both formed and one is selected.  Every value is written
+// to the row (unknown ones are rewritten by the fix-up pass before anything
+// reads them: the only same-row reads are of pixels 0..2, which lane 0 -- exact
+// from the start -- writes at its steps 0..2, before the last segment reaches
+// its last three columns; the host keeps that segment >= 6 pixels long).
+// Returns the last segment-local index left unknown (-1: none).
+__device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, const uint32_t* recs,
+                                           uint32_t x0, uint32_t x_stop, IvS r0, IvS r1, IvS r2) {
   int last_unknown = -1;
   const uint32_t y = rc.y;
+  const uint32_t W = rc.W;
   uint32_t* row = rc.row(y);
-  const uint32_t* up = y > 0 ? rc.row(y - 1) : nullptr;
-  uint32_t x = x0;
-  // ---- interval phase
-  while (x < x_stop && !(px_exact(r0) && px_exact(r1) && px_exact(r2))) {
+  const uint32_t* up = rc.row(y - 1);       // unused on row 0
+  const bool has_up = y > 0;
+  for (uint32_t x = x0; x < x_stop; ++x) {
     const uint32_t r = recs[x];
-    Px3 v;
-    if (r == REC_RUN) {
-      v = r0;
-    } else if (!(r & REC_REF)) {
-      v = y > 0 ? px_avg(r0, up[x], r) : px_add(r0, r);
-    } else {
-      const int id = (int)((r >> 24) & 15u);
-      const int64_t off = L.ref_off[id];
-      Px3 src;
-      if (off == 0) src = px_from(0u);       // the pixel itself, not yet written (zeroed)
-      else if (off == 1) src = r0;
-      else if (off == 2) src = r1;
-      else if (off == 3) src = r2;
-      else {
-        uint32_t u;
-        src = ref_lookup(rc, x, L.ref_k[id], L.ref_d[id], &u) ? px_from(u) : px_unknown();
-      }
-      v = px_add(src, r);
+    const uint32_t u = up[x];
+    const bool run = r == REC_RUN;
+    const bool ref = !run && (r & REC_REF);
+    const uint32_t c = run ? 0u : spread3(r);
+    // reference value (kind REF): recent pixels or a pixel of the ring
+    const int id = (int)((r >> 24) & 15u);
+    const int off = (int)L.ref_off32[id];
+    int jx = (int)x - L.ref_d[id];
+    int jy = (int)y - L.ref_k[id];
+    if (W >= 4) {                 // one wrap at most (|d| <= 3)
+      const int wrapl = jx < 0, wrapr = jx >= (int)W;
+      jx += wrapl ? (int)W : (wrapr ? -(int)W : 0);
+      jy += wrapr - wrapl;
+    } else {                      // tiny widths: general linear index
+      const int64_t j = (int64_t)y * W + x - ((int64_t)L.ref_k[id] * W + L.ref_d[id]);
+      const int64_t jj = j < 0 ? 0 : j;
+      jy = (int)(jj / W);
+      jx = (int)(jj - (int64_t)jy * W);
     }
-    if (px_exact(v)) row[x] = pack_px(v);
-    else last_unknown = (int)(x - x0);
+    jx = min(max(jx, 0), (int)W - 1);
+    const uint32_t far = (jy + 4 == (int)y && rc.rmask == 3u)
+                             ? rc.y4tail[max(jx - (int)(W - 3), 0)]
+                             : rc.ring[(size_t)((uint32_t)jy & rc.rmask) * W + (uint32_t)jx];
+    IvS src;
+    src.lo = off == 1 ? r0.lo : off == 2 ? r1.lo : off == 3 ? r2.lo : off == 0 ? 0u : far;
+    src.len = off == 1 ? r0.len : off == 2 ? r1.len : off == 3 ? r2.len : 0u;
+    src = ref ? src : r0;
+    const IvS va = ivs_avg(r0, u, c);
+    const IvS vr = ivs_add(src, c);
+    const bool avg = !run && !ref && has_up;
+    const IvS v{avg ? va.lo : vr.lo, avg ? va.len : vr.len};
+    row[x] = v.lo;
+    last_unknown = v.len ? (int)(x - x0) : last_unknown;
     r2 = r1; r1 = r0; r0 = v;
-    ++x;
-  }
-  // ---- exact phase
-  uint32_t p1 = pack_px(r0), p2 = pack_px(r1), p3 = pack_px(r2);
-  for (; x < x_stop; ++x) {
-    const uint32_t r = recs[x];
-    uint32_t v;
-    if (r == REC_RUN) {
-      v = p1;
-    } else if (!(r & REC_REF)) {
-      v = add_rgb(y > 0 ? avg_rgb(p1, up[x]) : p1, r);
-    } else {
-      const int id = (int)((r >> 24) & 15u);
-      const int64_t off = L.ref_off[id];
-      uint32_t src;
-      if (off == 0) src = 0u;
-      else if (off == 1) src = p1;
-      else if (off == 2) src = p2;
-      else if (off == 3) src = p3;
-      else if (!ref_lookup(rc, x, L.ref_k[id], L.ref_d[id], &src)) {
-        // a same-row pixel another lane has not written yet: leave the rest of
-        // the segment to the exact fix-up pass
-        last_unknown = (int)(x_stop - 1 - x0);
-        break;
-      }
-      v = add_rgb(src, r);
-    }
-    row[x] = v;
-    if (x < 3) atomicOr(first3, 1u << x);
-    p3 = p2; p2 = p1; p1 = v;
   }
   return last_unknown;
 }
@@ -653,7 +606,8 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   if (lane < 16) {
     L.ref_k[lane] = ref_rows(lane);
     L.ref_d[lane] = ref_px_off(lane);
-    L.ref_off[lane] = (int64_t)ref_rows(lane) * W + ref_px_off(lane);
+    const int64_t off = (int64_t)ref_rows(lane) * W + ref_px_off(lane);
+    L.ref_off32[lane] = (int32_t)(off < 0 ? 4 : off > 4 ? 4 : off);
   }
   if (lane == 0) L.err = 0;
   __syncthreads();
@@ -665,15 +619,14 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   const uint8_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 255 : 0;
   const bool active = (uint32_t)lane < nseg;
   const uint32_t x0 = lane * S;
-  const uint32_t x1 = active ? min(x0 + S, W) : x0;
+  const uint32_t x1 = active ? ((uint32_t)lane == nseg - 1 ? W : x0 + S) : x0;
   const uint32_t seglen = x1 - x0;
 
   unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0;
   for (uint32_t y = 0; y < H; ++y) {
     const unsigned long long c0 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
-    RowCtx rc{ring, L.y4tail, &L.first3, W, y, R - 1, x0, true};
+    RowCtx rc{ring, L.y4tail, W, y, R - 1};
     if (R == 4 && y >= 4 && lane < 3) L.y4tail[lane] = rc.row(y)[W - 3 + lane];
-    if (lane == 0) L.first3 = 0;
     // this row's records, coalesced
     const uint32_t* rrow = recs + (uint64_t)y * W;
     for (uint32_t x = lane; x < W; x += 64) recbuf[x] = rrow[x];
@@ -683,18 +636,18 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
       const uint64_t jy = (uint64_t)j / W, jx = (uint64_t)j - jy * W;
       return (R == 4 && jy + 4 == y) ? L.y4tail[jx - (W - 3)] : rc.row((uint32_t)jy)[jx];
     };
-    Px3 r0, r1, r2;
+    IvS r0, r1, r2;
     if (lane == 0) {
-      r0 = px_from(linear_px((int64_t)y * W - 1));
-      r1 = px_from(linear_px((int64_t)y * W - 2));
-      r2 = px_from(linear_px((int64_t)y * W - 3));
+      r0 = ivs_exact(linear_px((int64_t)y * W - 1));
+      r1 = ivs_exact(linear_px((int64_t)y * W - 2));
+      r2 = ivs_exact(linear_px((int64_t)y * W - 3));
     } else {
-      r0 = px_unknown(); r1 = px_unknown(); r2 = px_unknown();
+      r0 = IvS{0u, SP_K}; r1 = r0; r2 = r0;
     }
     const unsigned long long c1 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // speculative pass: lane 0 starts exact, the others from an unknown entry
     int last_unknown = -1;
-    if (active) last_unknown = run_segment(rc, L, &L.first3, recbuf, x0, x1, r0, r1, r2);
+    if (active) last_unknown = run_segment(rc, L, recbuf, x0, x1, r0, r1, r2);
     // fix-up rounds: an unconverged segment is recomputed exactly as soon as the
     // three pixels before it are exact (left segment converged before its last
     // three pixels, or already fixed) -- normally all in one parallel round
@@ -709,17 +662,15 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
     if (a.stats && active && last_unknown >= 0) atomicAdd(&a.stats[3], (unsigned long long)(last_unknown + 1));
     __syncthreads();
     const unsigned long long c2 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
-    rc.spec = false;
     while (fin != ~0ull) {
       const bool mine = !((fin >> lane) & 1ull);
       const bool left_ok = lane == 0 || (((fin | tail_ok) >> (lane - 1)) & 1ull);
       const bool ready = mine && left_ok;
       if (ready) {
-        r0 = px_from(linear_px((int64_t)y * W + x0 - 1));
-        r1 = px_from(linear_px((int64_t)y * W + x0 - 2));
-        r2 = px_from(linear_px((int64_t)y * W + x0 - 3));
-        const int lu = run_segment(rc, L, &L.first3, recbuf, x0, x0 + (uint32_t)last_unknown + 1,
-                                   r0, r1, r2);
+        r0 = ivs_exact(linear_px((int64_t)y * W + x0 - 1));
+        r1 = ivs_exact(linear_px((int64_t)y * W + x0 - 2));
+        r2 = ivs_exact(linear_px((int64_t)y * W + x0 - 3));
+        const int lu = run_segment(rc, L, recbuf, x0, x0 + (uint32_t)last_unknown + 1, r0, r1, r2);
         if (lu >= 0) atomicCAS(&L.err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         last_unknown = -1;
       }
@@ -736,10 +687,10 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
     const uint32_t* row = rc.row(y);
     if (OC == 4) {
       uint32_t* o32 = reinterpret_cast<uint32_t*>(orow);
-      for (uint32_t x = lane; x < W; x += 64) o32[x] = row[x] | ((uint32_t)alpha << 24);
+      for (uint32_t x = lane; x < W; x += 64) o32[x] = unspread3(row[x]) | ((uint32_t)alpha << 24);
     } else {
       for (uint32_t x = lane; x < W; x += 64) {
-        const uint32_t v = row[x];
+        const uint32_t v = unspread3(row[x]);
         uint8_t* o = orow + (uint64_t)x * 3;
         o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16);
       }

@@ -483,245 +483,270 @@ __device__ __forceinline__ void or_bits(uint32_t* buf, uint64_t pos, uint32_t v,
   }
 }
 
+// Wave-parallel decoupled look-back for tile t (wave 0 only): lane i inspects
+// predecessor t-1-i; a window without an inclusive prefix folds 64 aggregates
+// and moves back 64 tiles.  Returns the exclusive (bit length, last 32 bits).
+__device__ inline void look_back(const EncArgs& a, uint64_t t, uint32_t tt, uint32_t f, int lane,
+                                 uint64_t* wlen, uint32_t* wsuf, uint64_t* out_len, uint32_t* out_suf) {
+  TileDesc* desc = reinterpret_cast<TileDesc*>(a.tiles_desc);
+  const int64_t fs = (int64_t)t - tt;           // first tile of this frame
+  uint64_t acc_len = 0;                         // tiles (base+1 .. t-1), concatenated
+  uint32_t acc_suf = 0;
+  int64_t base = (int64_t)t - 1;
+  uint32_t spins = 0;
+  while (true) {
+    const int64_t j = base - lane;
+    uint64_t st, len;
+    uint32_t suf = 0;
+    if (j < fs) {                               // before the frame: the header seed
+      st = ST_INC;
+      len = a.seed_bit[f];
+    } else {
+      const unsigned long long fl = ld_rlx64(&desc[j].flag);
+      st = fl & ~LEN_MASK;
+      len = fl & LEN_MASK;
+    }
+    const unsigned long long inc = __ballot(st == ST_INC);
+    const int first_inc = inc ? __builtin_ctzll(inc) : 64;
+    const unsigned long long need = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1ull);
+    if (__ballot(st == 0) & need) {
+      if (++spins > 16) __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (lane <= first_inc) {
+      if (j < fs) suf = a.seed_suf[f];
+      else suf = st == ST_INC ? ld_rlx(&desc[j].suf_inc) : ld_rlx(&desc[j].suf_agg);
+      wlen[lane] = len;
+      wsuf[lane] = suf;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane == 0) {
+      const int last = first_inc < 64 ? first_inc : 63;
+      uint64_t l = 0;
+      uint32_t sx = 0;
+      for (int i = last; i >= 0; --i) suf_combine(l, sx, wlen[i], wsuf[i]);   // oldest first
+      suf_combine(l, sx, acc_len, acc_suf);
+      acc_len = l;
+      acc_suf = sx;
+    }
+    acc_len = __shfl(acc_len, 0);
+    acc_suf = __shfl(acc_suf, 0);
+    if (first_inc < 64) break;
+    base -= 64;
+  }
+  *out_len = acc_len;
+  *out_suf = acc_suf;
+}
+
+// Persistent: each block takes tiles in ticket order (forward progress for the
+// look-back), reloading the code table only when the frame changes.
 __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
   __shared__ TileWin tw;
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
+  __shared__ uint64_t wlen[64];
+  __shared__ uint32_t wsuf[64];
   __shared__ uint32_t s_tile;
   __shared__ uint64_t s_excl_len;
   __shared__ uint32_t s_excl_suf;
 
-  if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
-  __syncthreads();
-  const uint64_t t = s_tile;
-  const uint32_t T = a.tiles_per_frame;
-  const uint32_t f = (uint32_t)(t / T);
-  const uint32_t tt = (uint32_t)(t % T);
-  if (f >= a.n_frames) return;
-  if (a.frame_flags[f] & FLAG_SERIAL) return;   // whole frame handled by enc_serial
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const uint8_t* frame = a.px + (uint64_t)f * a.frame_stride;
-  const int64_t start = (int64_t)tt * ENC_TILE;
+  const uint32_t T = a.tiles_per_frame;
+  const uint64_t total = (uint64_t)a.n_frames * T;
   const int64_t N = (int64_t)a.W * a.H;
-  const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+  uint32_t cur_f = 0xFFFFFFFFu;
+  uint32_t used_words = PACK_MAX_WORDS;        // bits[] words to clear before the next tile
+  TileDesc* descs = reinterpret_cast<TileDesc*>(a.tiles_desc);
 
-  for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
-  for (int w = threadIdx.x; w < PACK_MAX_WORDS; w += ENC_THREADS) bits[w] = 0;
-  stage_tile(tw, frame, start, N, a.W, a.C);
-  __syncthreads();
-
-  uint32_t coded_bits = 0;
-#pragma unroll
-  for (int r = 0; r < PX_PER_THREAD; ++r) {
-    const int p = r * ENC_THREADS + threadIdx.x;
-    const int64_t i = start + p;
-    bool coded = false;
-    if (p < count) coded = (i == 0) || (tw.w[0][p + 3] != tw.w[0][p + 2]);
-    const unsigned long long bal = __ballot(coded);
-    if (lane == 0) {
-      const int wbase = (r * ENC_THREADS + (threadIdx.x & ~63)) >> 5;
-      mask[wbase] = (uint32_t)bal;
-      mask[wbase + 1] = (uint32_t)(bal >> 32);
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+    for (uint32_t w = threadIdx.x; w < used_words; w += ENC_THREADS) bits[w] = 0;
+    __syncthreads();
+    const uint64_t t = s_tile;
+    if (t >= total) break;
+    const uint32_t f = (uint32_t)(t / T);
+    const uint32_t tt = (uint32_t)(t % T);
+    if (a.frame_flags[f] & FLAG_SERIAL) { used_words = 0; continue; }   // enc_serial's frame
+    const uint8_t* frame = a.px + (uint64_t)f * a.frame_stride;
+    const int64_t start = (int64_t)tt * ENC_TILE;
+    const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+    if (f != cur_f) {
+      for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
+      cur_f = f;
     }
-    coded_bits |= (coded ? 1u : 0u) << r;
-  }
-  __syncthreads();
+    stage_tile(tw, frame, start, N, a.W, a.C);
+    __syncthreads();
 
-  const bool fast = (a.W >= 3) && (start >= 3 * (int64_t)a.W + 3);
-  const uint32_t next_tile_px = a.tile_next[t];
-  PixSyms sy[PX_PER_THREAD];
-  uint64_t runs[PX_PER_THREAD];
-  uint32_t nb[PX_PER_THREAD];
-  uint32_t my_total = 0;
+    uint32_t coded_bits = 0;
 #pragma unroll
-  for (int r = 0; r < PX_PER_THREAD; ++r) {
-    const int p = r * ENC_THREADS + threadIdx.x;
-    nb[r] = 0;
-    runs[r] = 0;
-    sy[r].n = 0;
-    if ((coded_bits >> r) & 1u) {
-      WinAcc acc{&tw, p + 3};
-      if (fast) classify<true>((uint32_t)(start + p), a.W, acc, sy[r]);
-      else classify<false>((uint32_t)(start + p), a.W, acc, sy[r]);
-      uint32_t n = tbl[BIN_PREFIX + sy[r].mode] & 31u;
+    for (int r = 0; r < PX_PER_THREAD; ++r) {
+      const int p = r * ENC_THREADS + threadIdx.x;
+      const int64_t i = start + p;
+      bool coded = false;
+      if (p < count) coded = (i == 0) || (tw.w[0][p + 3] != tw.w[0][p + 2]);
+      const unsigned long long bal = __ballot(coded);
+      if (lane == 0) {
+        const int wbase = (r * ENC_THREADS + (threadIdx.x & ~63)) >> 5;
+        mask[wbase] = (uint32_t)bal;
+        mask[wbase + 1] = (uint32_t)(bal >> 32);
+      }
+      coded_bits |= (coded ? 1u : 0u) << r;
+    }
+    __syncthreads();
+
+    const bool fast = (a.W >= 3) && (start >= 3 * (int64_t)a.W + 3);
+    const uint32_t next_tile_px = a.tile_next[t];
+    uint32_t round_base = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((uint32_t)k < sy[r].n) n += tbl[sy[r].b[k]] & 31u;
-      const int nx = next_coded_local(mask, p);
-      const uint64_t nxt = (nx < count) ? (uint64_t)(start + nx) : (uint64_t)next_tile_px;
-      const uint64_t run = nxt - (uint64_t)(start + p) - 1;
-      runs[r] = run;
-      if (run > 0) {
-        uint64_t m = run - 1;
-        while (true) {
-          n += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
-          if (m < 8) break;
-          m >>= 3;
+    for (int r = 0; r < PX_PER_THREAD; ++r) {
+      const int p = r * ENC_THREADS + threadIdx.x;
+      PixSyms sy;
+      sy.n = 0;
+      sy.mode = 0;
+      uint64_t run = 0;
+      uint32_t nb = 0;
+      if ((coded_bits >> r) & 1u) {
+        WinAcc acc{&tw, p + 3};
+        if (fast) classify<true>((uint32_t)(start + p), a.W, acc, sy);
+        else classify<false>((uint32_t)(start + p), a.W, acc, sy);
+        nb = tbl[BIN_PREFIX + sy.mode] & 31u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((uint32_t)k < sy.n) nb += tbl[sy.b[k]] & 31u;
+        const int nx = next_coded_local(mask, p);
+        const uint64_t nxt = (nx < count) ? (uint64_t)(start + nx) : (uint64_t)next_tile_px;
+        run = nxt - (uint64_t)(start + p) - 1;
+        if (run > 0) {
+          uint64_t m = run - 1;
+          while (true) {
+            nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
+            if (m < 8) break;
+            m >>= 3;
+          }
         }
       }
-      nb[r] = n;
-    }
-    my_total += nb[r];
-  }
-  // block exclusive scan of per-thread totals (threads in order of... pixel order is
-  // r-major, so scan per round r over the block, chaining rounds).
-  // Simple approach: per-round block scans.
-  uint32_t excl[PX_PER_THREAD];
-  uint32_t round_base = 0;
+      // block-wide exclusive scan of this round's pixel bit lengths
+      uint32_t x = nb;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y2 = __shfl_up(x, o);
+        if (lane >= o) x += y2;
+      }
+      if (lane == 63) wsum[wid] = x;
+      __syncthreads();
+      uint32_t wbase = 0, rtotal = 0;
 #pragma unroll
-  for (int r = 0; r < PX_PER_THREAD; ++r) {
-    uint32_t v = nb[r];
-    // inclusive wave scan
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    uint32_t wbase = 0, rtotal = 0;
-    for (int w = 0; w < ENC_THREADS / 64; ++w) {
-      if (w < wid) wbase += wsum[w];
-      rtotal += wsum[w];
-    }
-    excl[r] = round_base + wbase + x - v;
-    round_base += rtotal;
-    __syncthreads();
-  }
-  const uint32_t tile_bits = round_base;
-
-  // assemble local bits (MSB-first) into LDS
-#pragma unroll
-  for (int r = 0; r < PX_PER_THREAD; ++r) {
-    if (!((coded_bits >> r) & 1u)) continue;
-    uint64_t pos = excl[r];
-    uint32_t e = tbl[BIN_PREFIX + sy[r].mode];
-    or_bits(bits, pos, e >> 5, e & 31u);
-    pos += e & 31u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if ((uint32_t)k < sy[r].n) {
-        e = tbl[sy[r].b[k]];
+      for (int w = 0; w < ENC_THREADS / 64; ++w) {
+        const uint32_t ws = wsum[w];
+        wbase += (w < wid) ? ws : 0u;
+        rtotal += ws;
+      }
+      const uint32_t excl = round_base + wbase + x - nb;
+      round_base += rtotal;
+      __syncthreads();
+      // assemble this pixel's bits (MSB-first) into the tile buffer
+      if (nb) {
+        uint64_t pos = excl;
+        uint32_t e = tbl[BIN_PREFIX + sy.mode];
         or_bits(bits, pos, e >> 5, e & 31u);
         pos += e & 31u;
-      }
-    }
-    if (runs[r] > 0) {
-      uint64_t m = runs[r] - 1;
-      while (true) {
-        e = tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
-        or_bits(bits, pos, e >> 5, e & 31u);
-        pos += e & 31u;
-        if (m < 8) break;
-        m >>= 3;
-      }
-    }
-  }
-  __syncthreads();
-
-  // local last-32-bits
-  TileDesc* desc = reinterpret_cast<TileDesc*>(a.tiles_desc) + t;
-  if (threadIdx.x == 0) {
-    uint32_t suf = 0;
-    if (tile_bits > 0) {
-      const uint32_t endw = (tile_bits - 1) >> 5;   // word holding the last bit
-      const uint32_t o = tile_bits & 31;            // bits used in the last word (0 => 32)
-      if (o == 0) suf = bits[endw];
-      else {
-        const uint32_t lo = bits[endw] >> (32 - o);
-        const uint32_t hi = endw ? bits[endw - 1] : 0u;
-        suf = (hi << o) | lo;
-      }
-      if (tile_bits < 32) suf &= (1u << tile_bits) - 1u;
-    }
-    uint64_t excl_len;
-    uint32_t excl_suf;
-    if (tt == 0) {
-      excl_len = a.seed_bit[f];
-      excl_suf = a.seed_suf[f];
-    } else {
-      st_rlx(&desc->suf_agg, suf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_rlx64(&desc->flag, ST_AGG | tile_bits);
-      // look-back, one lane (tiles are ~1K px; chains are short)
-      excl_len = 0;
-      excl_suf = 0;
-      // accumulate predecessor aggregates in reverse, then combine in order
-      uint64_t acc_len = 0;
-      uint32_t acc_suf = 0;   // suffix of the concatenation of visited predecessors
-      int64_t j = (int64_t)t - 1;
-      uint32_t spins = 0;
-      while (true) {
-        TileDesc* pd = reinterpret_cast<TileDesc*>(a.tiles_desc) + j;
-        const unsigned long long fl = ld_rlx64(&pd->flag);
-        const uint64_t st = fl & ~LEN_MASK;
-        if (st == 0) { if (++spins > 64) __builtin_amdgcn_s_sleep(1); continue; }
-        const uint64_t len = fl & LEN_MASK;
-        if (st == ST_INC) {
-          const uint32_t ps = ld_rlx(&pd->suf_inc);
-          // result = pred_inclusive ++ acc
-          uint64_t l = len;
-          uint32_t sfx = ps;
-          suf_combine(l, sfx, acc_len, acc_suf);
-          excl_len = l;
-          excl_suf = sfx;
-          break;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if ((uint32_t)k < sy.n) {
+            e = tbl[sy.b[k]];
+            or_bits(bits, pos, e >> 5, e & 31u);
+            pos += e & 31u;
+          }
         }
-        const uint32_t ps = ld_rlx(&pd->suf_agg);
-        // acc = pred_agg ++ acc
-        uint64_t l = len;
-        uint32_t sfx = ps;
-        suf_combine(l, sfx, acc_len, acc_suf);
-        acc_len = l;
-        acc_suf = sfx;
-        --j;
+        if (run > 0) {
+          uint64_t m = run - 1;
+          while (true) {
+            e = tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
+            or_bits(bits, pos, e >> 5, e & 31u);
+            pos += e & 31u;
+            if (m < 8) break;
+            m >>= 3;
+          }
+        }
       }
     }
-    uint64_t inc_len = excl_len;
-    uint32_t inc_suf = excl_suf;
-    suf_combine(inc_len, inc_suf, tile_bits, suf);
-    st_rlx(&desc->suf_inc, inc_suf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_rlx64(&desc->flag, ST_INC | inc_len);
-    s_excl_len = excl_len;
-    s_excl_suf = excl_suf;
-  }
-  __syncthreads();
-  const uint64_t s0 = s_excl_len;
-  const uint32_t suf0 = s_excl_suf;
-  const uint64_t e0 = s0 + tile_bits;
-  const uint64_t w0 = s0 >> 5, w1 = e0 >> 5;
-  const uint32_t sh = (uint32_t)(s0 & 31);
-  uint8_t* out = a.out + (uint64_t)f * a.out_stride;
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
-  // word w0+m = (prev : bits[m]) >> sh, prev = bits[m-1] or suffix for m == 0
-  for (uint64_t m = threadIdx.x; m < w1 - w0; m += ENC_THREADS) {
-    const uint32_t hi = m ? bits[m - 1] : suf0;
-    const uint32_t lo = bits[m];
-    const uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
-    out32[w0 + m] = __builtin_bswap32(v);
-  }
-  if (tt == T - 1 && threadIdx.x == 0) {
-    // tail: partial word w1, then [P, P, 0, 0, 0] (hfe.rs:115, code.rs:421-422)
-    const uint64_t m = w1 - w0;
-    const uint32_t hi = m ? bits[m - 1] : suf0;
-    const uint32_t lo = bits[m];
-    uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
-    const uint32_t q = (uint32_t)(e0 & 31);
-    v = q ? (v & (0xFFFFFFFFu << (32 - q))) : 0u;
-    const uint64_t B = e0 >> 3;              // index of the partial/cache byte
-    uint64_t p = w1 * 4;
-    for (; p < B; ++p) out[p] = (uint8_t)(v >> (24 - 8 * (p - w1 * 4)));
-    const uint8_t P = (e0 & 7) ? (uint8_t)(v >> (24 - 8 * (B - w1 * 4))) : 0u;
-    out[B] = P;
-    out[B + 1] = P;
-    out[B + 2] = 0;
-    out[B + 3] = 0;
-    out[B + 4] = 0;
-    a.out_len[f] = B + 5;
+    const uint32_t tile_bits = round_base;
+    __syncthreads();
+
+    if (wid == 0) {
+      // local last 32 bits
+      uint32_t suf = 0;
+      if (tile_bits > 0) {
+        const uint32_t endw = (tile_bits - 1) >> 5;
+        const uint32_t o = tile_bits & 31;
+        if (o == 0) suf = bits[endw];
+        else suf = ((endw ? bits[endw - 1] : 0u) << o) | (bits[endw] >> (32 - o));
+        if (tile_bits < 32) suf &= (1u << tile_bits) - 1u;
+      }
+      TileDesc* desc = descs + t;
+      uint64_t excl_len;
+      uint32_t excl_suf;
+      if (tt == 0) {
+        excl_len = a.seed_bit[f];
+        excl_suf = a.seed_suf[f];
+      } else {
+        if (lane == 0) {
+          st_rlx(&desc->suf_agg, suf);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          st_rlx64(&desc->flag, ST_AGG | tile_bits);
+        }
+        look_back(a, t, tt, f, lane, wlen, wsuf, &excl_len, &excl_suf);
+      }
+      if (lane == 0) {
+        uint64_t inc_len = excl_len;
+        uint32_t inc_suf = excl_suf;
+        suf_combine(inc_len, inc_suf, tile_bits, suf);
+        st_rlx(&desc->suf_inc, inc_suf);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_rlx64(&desc->flag, ST_INC | inc_len);
+        s_excl_len = excl_len;
+        s_excl_suf = excl_suf;
+      }
+    }
+    __syncthreads();
+    const uint64_t s0 = s_excl_len;
+    const uint32_t suf0 = s_excl_suf;
+    const uint64_t e0 = s0 + tile_bits;
+    const uint64_t w0 = s0 >> 5, w1 = e0 >> 5;
+    const uint32_t sh = (uint32_t)(s0 & 31);
+    uint8_t* out = a.out + (uint64_t)f * a.out_stride;
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+    // word w0+m = (prev : bits[m]) >> sh, prev = bits[m-1] or the exclusive suffix
+    for (uint64_t m = threadIdx.x; m < w1 - w0; m += ENC_THREADS) {
+      const uint32_t hi = m ? bits[m - 1] : suf0;
+      const uint32_t lo = bits[m];
+      const uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+      out32[w0 + m] = __builtin_bswap32(v);
+    }
+    if (tt == T - 1 && threadIdx.x == 0) {
+      // tail: partial word w1, then [P, P, 0, 0, 0] (hfe.rs:115, code.rs:421-422)
+      const uint64_t m = w1 - w0;
+      const uint32_t hi = m ? bits[m - 1] : suf0;
+      const uint32_t lo = bits[m];
+      uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+      const uint32_t q = (uint32_t)(e0 & 31);
+      v = q ? (v & (0xFFFFFFFFu << (32 - q))) : 0u;
+      const uint64_t B = e0 >> 3;              // index of the partial/cache byte
+      uint64_t pp = w1 * 4;
+      for (; pp < B; ++pp) out[pp] = (uint8_t)(v >> (24 - 8 * (pp - w1 * 4)));
+      const uint8_t P = (e0 & 7) ? (uint8_t)(v >> (24 - 8 * (B - w1 * 4))) : 0u;
+      out[B] = P;
+      out[B + 1] = P;
+      out[B + 2] = 0;
+      out[B + 3] = 0;
+      out[B + 4] = 0;
+      a.out_len[f] = B + 5;
+    }
+    used_words = (uint32_t)(w1 - w0 + 2);
   }
 }
 
