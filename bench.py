@@ -85,12 +85,47 @@ def cpu_baseline(W, H, seconds=12.0):
                       f"{t_total:.1f} s single-thread"}
 
 
+def timed_region(step, steps, sync, barrier):
+    """Barrier + sync on both sides of exactly `steps` calls of `step`."""
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(value, dist, device):
+    """Whole-job time is the slowest rank's (RCCL all-reduce MAX; gloo in tests)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_traffic(kernel, frames, path=None):
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (bytes per
+    frame from separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected; see
+    profiles/README.md), scaled to this launch's frame count; None if absent."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return int(d["kernels"][kernel]["hbm_bytes_per_frame"] * frames)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=256, help="frames per step per GPU")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -138,24 +173,13 @@ def main():
     stream_bytes = int(lens.sum())
 
     L.nice_ctx_set_timing(ctx.ptr, 1)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
+    elapsed = timed_region(step, args.steps, torch.cuda.synchronize, barrier)
     ms = (ctypes.c_double * 12)()
     cnt = (ctypes.c_uint32 * 12)()
     L.nice_ctx_read_timing(ctx.ptr, ms, cnt)
     L.nice_ctx_set_timing(ctx.ptr, 0)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, device)
 
     # encode-only / decode-only rates (separate short runs, outside the main timing)
     def timed(fn, reps=2):
@@ -181,8 +205,8 @@ def main():
     out_px_bytes = F * N * 4
     algo = {
         "enc_classify": in_bytes, "enc_pack": in_bytes + stream_bytes,
-        "dec_sync": stream_bytes, "dec_count": stream_bytes, "dec_bounds": stream_bytes,
-        "dec_reconstruct": stream_bytes + out_px_bytes,
+        "dec_sync": stream_bytes, "dec_emit": stream_bytes,
+        "dec_reconstruct": out_px_bytes,
     }
     dom = max((k for k in phase if k in algo), key=lambda k: phase[k]["ms_total"])
     avg_s = phase[dom]["ms_total"] / 1e3 / phase[dom]["launches"]
@@ -208,9 +232,13 @@ def main():
                    "parallelism": f"frames sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": round(achieved * 1e9 / HBM_PEAK, 5), "traffic": None,
+                     "frac": round(achieved * 1e9 / HBM_PEAK, 5),
+                     "traffic": load_traffic(dom, F),
                      "algo_bytes_per_launch": algo[dom],
                      "avg_launch_ms": round(avg_s * 1e3, 4)},
+        # whole path against HBM: encode (px in + stream out) + decode (stream in + px out)
+        "path_roofline_frac": round(2 * (in_bytes + stream_bytes) / (elapsed / args.steps)
+                                    / HBM_PEAK * world, 5),
         "encode_mpix_s": round(F * N / t_enc / 1e6, 2),
         "decode_mpix_s": round(F * N / t_dec / 1e6, 2),
         "single_frame_latency_ms": round(t_one * 1e3, 2),

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import ROOT, nice_pkg
 
 
@@ -50,3 +52,21 @@ def test_no_oracle_in_product():
                 text = open(os.path.join(dirpath, f)).read()
                 assert "liboracle" not in text and "nice_oracle" not in text, f
                 assert "from oracle" not in text and "import oracle" not in text, f
+
+
+def test_cpp_mirror_compiles(tmp_path):
+    """include/nice.hpp (C++ mirror of code::encode/decode) compiles against nice.h
+    and links libnice_hip.so with plain g++."""
+    import subprocess
+    subprocess.check_call(["make", "-s", "-B", "-C", os.path.join(ROOT, "examples"), "roundtrip"])
+    assert os.path.exists(os.path.join(ROOT, "examples", "roundtrip"))
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_roundtrip():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "examples"), "roundtrip"])
+    out = subprocess.run([os.path.join(ROOT, "examples", "roundtrip"), "1283", "719"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("ok")

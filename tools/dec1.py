@@ -1,7 +1,7 @@
 """Diagnostic: decode one 4K RGBA SYN-v1 stream through the product path."""
 import importlib, os, sys
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
 from oracle import oracle as O
 w, h = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))

@@ -1,7 +1,7 @@
 """Diagnostic: encode N 4K RGBA SYN-v1 frames through the device batch path."""
 import importlib, os, sys
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
 from oracle import oracle as O

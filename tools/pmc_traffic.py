@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from two rocprofv3 counter passes (FETCH_SIZE and
+WRITE_SIZE cannot share a pass on gfx950, MI355X_MICROARCH.md "rocprofv3 PMC
+slots").  FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half
+the bytes of a wide coalesced read, so it is doubled (MI355X_MICROARCH.md
+"HBM").  Output: bytes per dispatch and per frame for each kernel.
+
+    python tools/pmc_traffic.py FRAMES fetch_counter_collection.csv \
+        write_counter_collection.csv > profiles/pmc_traffic_r01.json
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = re.split(r"[(<]", r["Kernel_Name"])[0].strip()
+        if name.startswith("__amd") or not name:
+            continue
+        acc[name].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def main():
+    frames = int(sys.argv[1])
+    fetch = per_kernel(sys.argv[2], "FETCH_SIZE")
+    write = per_kernel(sys.argv[3], "WRITE_SIZE")
+    out = {"frames_per_dispatch": frames,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes; "
+                     "KiB -> bytes; FETCH_SIZE x2 (gfx950 half-count of wide reads)",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, (0.0, 0))[0] * 1024 * 2
+        w = write.get(k, (0.0, 0))[0] * 1024
+        out["kernels"][k] = {"dispatches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1]),
+                             "read_bytes_per_dispatch": int(f), "write_bytes_per_dispatch": int(w),
+                             "hbm_bytes_per_frame": int((f + w) / frames)}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
