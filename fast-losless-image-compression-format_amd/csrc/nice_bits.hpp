@@ -32,8 +32,9 @@ struct DecTables {
   uint8_t len[N_BINS];
   uint8_t max_aob[N_STREAMS];
   uint8_t lut_bits[N_STREAMS];
-  uint8_t pad[12];
+  uint8_t pad[18];
 };
+static_assert(sizeof(DecTables) % 16 == 0, "per-frame tables stay 16-byte aligned");
 
 struct BitSrc {
   const uint8_t* p;
@@ -82,63 +83,6 @@ __device__ __forceinline__ uint32_t dec_symbol(const BitSrc& src, const Tab& t, 
   return t.sym[lo];
 }
 
-// Thread-private MSB-first reader: a 64-bit window of two big-endian words plus
-// one prefetched word, so decoding a symbol costs a table lookup and, every
-// ~32 bits, one global load issued a word ahead of its use.
-struct LaneBits {
-  const uint8_t* p;
-  uint64_t len;      // bytes
-  uint64_t pos;      // absolute bit position
-  uint64_t wi;       // window = words [wi, wi+1]
-  uint64_t win;
-  uint32_t nxt;      // word wi+2
-  __device__ __forceinline__ uint32_t word(uint64_t j) const {
-    if ((j + 1) * 4 <= len) return __builtin_bswap32(reinterpret_cast<const uint32_t*>(p)[j]);
-    uint32_t v = 0;
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t i = j * 4 + k;
-      v = (v << 8) | (i < len ? p[i] : (len ? p[len - 1] : 0u));
-    }
-    return v;
-  }
-  __device__ __forceinline__ void seek(uint64_t bitpos) {
-    pos = bitpos;
-    wi = bitpos >> 5;
-    win = ((uint64_t)word(wi) << 32) | word(wi + 1);
-    nxt = word(wi + 2);
-  }
-  __device__ __forceinline__ uint32_t peek() const { return (uint32_t)((win << (pos & 31)) >> 32); }
-  __device__ __forceinline__ void skip(uint32_t n) {
-    pos += n;
-    if ((pos >> 5) != wi) {          // codes are <= 31 bits: at most one word per symbol
-      ++wi;
-      win = (win << 32) | nxt;
-      nxt = word(wi + 2);
-    }
-  }
-};
-
-template <class Tab>
-__device__ __forceinline__ uint32_t lane_symbol(LaneBits& br, const Tab& t, int s) {
-  const uint32_t v = br.peek();
-  const uint32_t lb = t.lut_bits[s];
-  const uint32_t e = t.lut[t.lut_off[s] + (v >> (32 - lb))];
-  if (e & 31u) {
-    br.skip(e & 31u);
-    return e >> 5;
-  }
-  const uint32_t mx = t.max_aob[s];
-  const uint32_t x = v >> (32 - mx);
-  int lo = stream_base(s), hi = stream_base(s) + stream_size(s) - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (t.lo[mid] <= x) hi = mid;
-    else lo = mid + 1;
-  }
-  br.skip(t.len[lo]);
-  return t.sym[lo];
-}
-
 // Decoder grammar (code.rs:576-671): gstate 0 expects a prefix; the payload
 // positions of each mode follow.
 //   BR 1 | RGB 2,3,4 | LUMA 5,6,7,8 | SD 9 | LUMA2 10,11,12
@@ -151,13 +95,5 @@ __host__ __device__ constexpr int gs_first(int mode) {
   return mode == P_BACK_REF ? 1 : mode == P_RGB ? 2 : mode == P_LUMA ? 5 : mode == P_SMALL_DIFF ? 9 : 10;
 }
 __host__ __device__ constexpr bool gs_last(int g) { return g == 1 || g == 4 || g == 8 || g == 9 || g == 12; }
-
-// Parse state between chunks.
-struct ParseState {
-  unsigned long long pos;  // absolute bit position of the next symbol
-  uint32_t g;              // grammar state
-  uint32_t dk;             // run digits read so far (0: no run in progress)
-  unsigned long long acc;  // run accumulator sum d_k << 3k
-};
 
 }  // namespace nice

@@ -78,8 +78,6 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T) {
   return L;
 }
 
-int g_device_ok = -1;
-
 int check_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return NICE_E_NODEV;
@@ -291,7 +289,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
 namespace {
 struct DecLayout {
   size_t total;
-  size_t o_tables, o_dstart, o_ea, o_eb, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
+  size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
 };
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint64_t npx, size_t rowbuf) {
   DecLayout L{};
@@ -299,11 +297,12 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint64_t npx, size_
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
   L.o_tables = take((size_t)n_frames * sizeof(DecTables));
   L.o_dstart = take((size_t)n_frames * 8);
-  L.o_ea = take((size_t)n_frames * max_chunks * sizeof(ParseState));
-  L.o_eb = take((size_t)n_frames * max_chunks * sizeof(ParseState));
+  L.o_entry = take((size_t)n_frames * max_chunks * 8);
+  L.o_last = take((size_t)n_frames * max_chunks * 8);
+  L.o_ck = take((size_t)n_frames * DEC_N_CK * max_chunks * 8);
   L.o_cpx = take((size_t)n_frames * max_chunks * 8);
   L.o_cstart = take((size_t)n_frames * max_chunks * 8);
-  L.o_recs = take((size_t)n_frames * npx * 4);
+  L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
   L.o_changed = take(16);
   L.o_rowbuf = take(rowbuf);
   L.total = o;
@@ -432,13 +431,15 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   a.chunk_blocks = (max_chunks + 255) / 256;
   a.chunk_px = (unsigned long long*)(base + L.o_cpx);
   a.chunk_start = (unsigned long long*)(base + L.o_cstart);
+  a.entry = (unsigned long long*)(base + L.o_entry);
+  a.last = (unsigned long long*)(base + L.o_last);
+  a.ck = (unsigned long long*)(base + L.o_ck);
   a.recs = (uint32_t*)(base + L.o_recs);
+  a.rec_stride = (N + 3) & ~3ull;
   a.seg = g.seg;
   a.nseg = g.nseg;
   a.rows_in_lds = g.in_lds ? 1u : 0u;
   a.rowbuf = (uint32_t*)(base + L.o_rowbuf);
-  ParseState* ea = (ParseState*)(base + L.o_ea);
-  ParseState* eb = (ParseState*)(base + L.o_eb);
   uint32_t* changed = (uint32_t*)(base + L.o_changed);
 
   PhaseTimer& tm = ctx->timer;
@@ -450,7 +451,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
     return NICE_OK;
   }
   hipLaunchKernelGGL(dec_init_entries, dim3((max_chunks + 255) / 256 < 64 ? (max_chunks + 255) / 256 : 64, n_frames),
-                     dim3(256), 0, st, a, ea);
+                     dim3(256), 0, st, a);
   const dim3 cgrid(n_frames * a.chunk_blocks);
   // Jacobi iteration of the chunk entry states to the fixpoint
   uint32_t host_changed = 1;
@@ -458,21 +459,18 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it, ++it_count) {
     NICE_HIP(hipMemsetAsync(changed, 0, 4, st));
     tm.begin(NICE_PH_DEC_SYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, (const ParseState*)ea, eb, changed);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed);
     tm.end(st);
     NICE_HIP(hipMemcpyAsync(&host_changed, changed, 4, hipMemcpyDeviceToHost, st));
     NICE_HIP(hipStreamSynchronize(st));
-    ParseState* t = ea;
-    ea = eb;
-    eb = t;
   }
   // the last sync iteration (no entry changed) already produced chunk_px
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
   tm.begin(NICE_PH_DEC_BOUNDS, st);
-  NICE_HIP(hipMemsetAsync(a.recs, 0xFF, (size_t)n_frames * N * 4, st));   // REC_RUN fill
-  hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a, (const ParseState*)ea);
+  NICE_HIP(hipMemsetAsync(a.recs, 0xFF, (size_t)n_frames * a.rec_stride * 4, st));   // REC_RUN fill
+  hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a);
   tm.end(st);
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,

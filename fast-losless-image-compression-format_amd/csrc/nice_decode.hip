@@ -12,9 +12,10 @@
 //                    decoded from a guessed entry state; exits become the next
 //                    slice's entry (Jacobi iteration) until a fixpoint -- Huffman
 //                    self-synchronisation makes this converge in a few passes.
-//   dec_count        pixels produced per chunk (coded pixels + run lengths).
-//   dec_scan         exclusive scan of those counts per frame.
-//   dec_bounds       parse state at every row-segment start (pixel y*W + s*SEG).
+//                    Re-parses stop at the first checkpoint where they agree
+//                    with the previous parse; the sync pass also counts pixels.
+//   dec_scan         exclusive scan of the pixel counts per frame.
+//   dec_emit         one 32-bit record per coded pixel (mode + constants).
 //   dec_reconstruct  one wave per frame, rows in order, one lane per row segment:
 //                    segments start from an unknown entry tracked as per-channel
 //                    cyclic intervals (exact once they collapse -- the predictors
@@ -176,42 +177,155 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
   if (threadIdx.x == 0) a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
 }
 
-// Table copy into LDS (all threads of the block participate).
-__device__ inline void load_tables(DecTables& dst, const DecTables* src) {
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-  uint32_t* d = reinterpret_cast<uint32_t*>(&dst);
-  for (uint32_t i = threadIdx.x; i < sizeof(DecTables) / 4; i += blockDim.x) d[i] = s[i];
+// ---------------------------------------------------------------------------
+// Parse machinery shared by dec_sync and dec_emit.
+//
+// One lane per 2048-bit chunk, 64 consecutive chunks per wave.  A lane reads
+// its bits from a private ring of RING_W big-endian words in LDS; the wave
+// refills all 64 rings together with 16-byte loads (consecutive lanes load
+// consecutive 16 bytes of one ring), so the stream is read from HBM in whole
+// lines instead of one 4-byte word per lane per load.  The first-level LUTs
+// live in LDS; long codes (rare: longer than the LUT width) take a search over
+// the canonical order in global memory (L2-resident).
+// ---------------------------------------------------------------------------
+constexpr uint32_t RING_W = 24;        // words per lane ring
+constexpr uint32_t RING_STRIDE = 28;   // words between rings (16-byte aligned)
+constexpr uint32_t RING_QUADS = RING_W / 4;
+
+struct LutLds {
+  uint16_t lut[DEC_LUT_BUDGET];
+  uint32_t gp[16];   // per grammar state: lut_off | lut_bits << 16 | stream << 24
+};
+
+__device__ inline void load_lut(LutLds& S, const DecTables* T) {
+  const uint4* s = reinterpret_cast<const uint4*>(T->lut);
+  uint4* d = reinterpret_cast<uint4*>(S.lut);
+  for (uint32_t i = threadIdx.x; i < sizeof(S.lut) / 16; i += blockDim.x) d[i] = s[i];
+  if (threadIdx.x < 13) {
+    const int st = gs_stream((int)threadIdx.x);
+    S.gp[threadIdx.x] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) | ((uint32_t)st << 24);
+  }
 }
 
-// One parse step (one symbol) of the grammar.  Updates the state and the pixel
-// contribution; returns the symbol.  Run digits contribute d << 3k (+1 for the
-// first digit), so per-chunk pixel counts are additive.
-template <class Tab>
-__device__ __forceinline__ uint32_t parse_step(LaneBits& br, const Tab& T, ParseState& ps,
-                                               uint64_t& px) {
-  const uint32_t sym = lane_symbol(br, T, gs_stream((int)ps.g));
-  ps.pos = br.pos;
-  if (ps.g == 0) {
-    if (sym >= (uint32_t)P_RUN1) {
-      const uint32_t d = sym - P_RUN1;
-      const uint32_t sh = (3u * ps.dk) & 63u;      // temp_curr_runcount u8 += 3, masked shift
-      px += ((uint64_t)d << sh) + (ps.dk == 0 ? 1u : 0u);
-      ps.acc += (uint64_t)d << sh;
-      ps.dk += 1;
+struct Lane {
+  unsigned long long pos;   // absolute bit position in the frame's stream
+  uint32_t wi;              // window = words wi, wi + 1
+  uint32_t ws;              // word held in ring[0]
+  unsigned long long win;
+  uint32_t nxt;             // word wi + 2
+  bool ok;                  // nxt valid: one more symbol may be decoded
+};
+
+__device__ __forceinline__ uint32_t stream_word(const uint8_t* p, uint64_t len, uint32_t w) {
+  uint32_t v = 0;
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t i = (uint64_t)w * 4 + k;
+    v = (v << 8) | (i < len ? p[i] : (len ? p[len - 1] : 0u));   // stale last byte past the end
+  }
+  return v;
+}
+
+// Wave-cooperative refill: every lane's ring restarts at its window word
+// (rounded down to 16 bytes).  Must be reached by all 64 lanes.
+__device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
+                                          Lane& L) {
+  const uint32_t lane = threadIdx.x & 63u;
+  L.ws = L.wi & ~3u;
+#pragma unroll
+  for (uint32_t r = 0; r < RING_QUADS; ++r) {
+    const uint32_t i = lane + 64u * r;
+    const uint32_t owner = i / RING_QUADS, q = i - owner * RING_QUADS;
+    const uint32_t w = (uint32_t)__shfl((int)L.ws, (int)owner) + 4u * q;
+    uint4 v;
+    if (al16 && ((uint64_t)w + 4) * 4 <= len) {
+      v = *reinterpret_cast<const uint4*>(p + (uint64_t)w * 4);
+      v.x = __builtin_bswap32(v.x); v.y = __builtin_bswap32(v.y);
+      v.z = __builtin_bswap32(v.z); v.w = __builtin_bswap32(v.w);
     } else {
-      px += 1;
-      ps.dk = 0;
-      ps.acc = 0;
-      ps.g = (uint32_t)gs_first((int)sym);
+      v.x = stream_word(p, len, w); v.y = stream_word(p, len, w + 1);
+      v.z = stream_word(p, len, w + 2); v.w = stream_word(p, len, w + 3);
     }
-  } else {
-    ps.g = gs_last((int)ps.g) ? 0u : ps.g + 1u;
+    *reinterpret_cast<uint4*>(wring + owner * RING_STRIDE + 4u * q) = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t* my = wring + lane * RING_STRIDE;
+  const uint32_t o = L.wi - L.ws;
+  L.win = ((unsigned long long)my[o] << 32) | my[o + 1];
+  L.nxt = my[o + 2];
+  L.ok = true;
+}
+
+__device__ __forceinline__ void lane_seek(Lane& L, unsigned long long pos) {
+  L.pos = pos;
+  L.wi = (uint32_t)(pos >> 5);
+  L.ok = false;
+}
+
+// One symbol of grammar state g (requires L.ok).
+__device__ __forceinline__ uint32_t ring_symbol(Lane& L, const uint32_t* my, const LutLds& S,
+                                                const DecTables* T, uint32_t g) {
+  const uint32_t v = (uint32_t)((L.win << (L.pos & 31u)) >> 32);
+  const uint32_t gp = S.gp[g];
+  const uint32_t lb = (gp >> 16) & 31u;
+  const uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - lb))];
+  uint32_t n = e & 31u, sym = e >> 5;
+  if (n == 0) {
+    const int s = (int)(gp >> 24);
+    const uint32_t x = v >> (32u - T->max_aob[s]);
+    int lo = stream_base(s), hi = stream_base(s) + stream_size(s) - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (T->lo[mid] <= x) hi = mid;
+      else lo = mid + 1;
+    }
+    n = T->len[lo];
+    sym = T->sym[lo];
+  }
+  L.pos += n;
+  if ((uint32_t)(L.pos >> 5) != L.wi) {   // codes are <= 31 bits: at most one word
+    ++L.wi;
+    L.win = (L.win << 32) | L.nxt;
+    const uint32_t o = L.wi + 2u - L.ws;
+    if (o < RING_W) L.nxt = my[o];
+    else L.ok = false;
   }
   return sym;
 }
 
-__device__ __forceinline__ bool state_eq(const ParseState& x, const ParseState& y) {
-  return x.pos == y.pos && x.g == y.g && x.dk == y.dk && x.acc == y.acc;
+// Grammar step (code.rs:576-671): g is the grammar state, dk the run digits
+// read so far (kept in 1..64 once nonzero: the reference's u8 shift counter
+// `+= 3` only matters mod 64), px the pixels this symbol accounts for (run
+// digit d contributes d << 3k, plus the run's first pixel on its first digit).
+constexpr uint32_t GS_FIRST = 1u | (2u << 4) | (5u << 8) | (9u << 12) | (10u << 16);
+constexpr uint32_t GS_LAST = (1u << 1) | (1u << 4) | (1u << 8) | (1u << 9) | (1u << 12);
+static_assert(P_BACK_REF == 0 && P_RGB == 1 && P_LUMA == 2 && P_SMALL_DIFF == 3 && P_LUMA2 == 4 &&
+                  P_RUN1 == 5, "prefix numbering");
+
+__device__ __forceinline__ uint32_t gstep(uint32_t sym, uint32_t& g, uint32_t& dk, uint64_t& px) {
+  if (g == 0) {
+    if (sym >= (uint32_t)P_RUN1) {
+      const uint32_t d = sym - P_RUN1;
+      px += ((uint64_t)d << ((3u * dk) & 63u)) + (dk == 0 ? 1u : 0u);
+      dk = dk >= 64u ? 1u : dk + 1u;
+    } else {
+      px += 1;
+      dk = 0;
+      g = (GS_FIRST >> (4u * sym)) & 15u;
+    }
+  } else {
+    g = ((GS_LAST >> g) & 1u) ? 0u : g + 1u;
+  }
+  return sym;
+}
+
+// Packed parse state: bit position relative to the data start (40 bits),
+// grammar state (4), run digits (7).  Bits 56..63 of `last` hold the number of
+// valid checkpoints.
+constexpr unsigned long long PS_MASK = (1ull << 51) - 1ull;
+__device__ __forceinline__ unsigned long long ps_pack(unsigned long long rel, uint32_t g, uint32_t dk) {
+  return rel | ((unsigned long long)g << 40) | ((unsigned long long)dk << 44);
 }
 
 // chunk geometry: chunk j of frame f covers bits [D + j*CB, D + (j+1)*CB)
@@ -221,25 +335,26 @@ __device__ __forceinline__ uint32_t n_chunks(uint64_t len, uint64_t D) {
 }
 
 // Initial entry guesses: every chunk starts at its first bit expecting a prefix.
-__global__ __launch_bounds__(256) void dec_init_entries(DecArgs a, ParseState* e) {
+__global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
   const uint32_t f = blockIdx.y;
-  const uint64_t D = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < a.max_chunks; j += gridDim.x * 256) {
-    ParseState& p = e[(uint64_t)f * a.max_chunks + j];
-    p.pos = D + (uint64_t)j * DEC_CHUNK_BITS;
-    p.g = 0;
-    p.dk = 0;
-    p.acc = 0;
+    const uint64_t i = (uint64_t)f * a.max_chunks + j;
+    a.entry[i] = ps_pack((unsigned long long)j * DEC_CHUNK_BITS, 0, 0);
+    a.last[i] = ~0ull;
   }
 }
 
 // ---------------------------------------------------------------------------
-// D1: sync iteration.  grid = n_frames * chunk_blocks, 256 threads, thread per
-// chunk.  Reads entries from `in`, writes exits into `out` (entry of j+1).
+// D1: sync iteration (Jacobi, in place).  Each lane parses its chunk from the
+// current entry guess and writes the exit as the next chunk's entry.  Lanes
+// whose entry did not change since their last parse do nothing.  A re-parse
+// compares its state with the previous parse at every CK_BITS checkpoint; once
+// they agree the rest of the chunk is unchanged (Huffman self-synchronisation),
+// so the lane stops and only patches its pixel count.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dec_sync(DecArgs a, const ParseState* in, ParseState* out,
-                                                uint32_t* changed) {
-  __shared__ DecTables T;
+__global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
+  __shared__ LutLds S;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
   const uint32_t f = blockIdx.x / a.chunk_blocks;
   const uint32_t jb = blockIdx.x % a.chunk_blocks;
   if (a.status[f] != 0) return;
@@ -247,61 +362,75 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, const ParseState* in,
   const uint64_t D = a.data_start[f];
   const uint32_t nc = n_chunks(len, D);
   if (jb * 256u >= nc) return;
-  load_tables(T, reinterpret_cast<const DecTables*>(a.tables) + f);
-  __syncthreads();
   const uint32_t j = jb * 256u + threadIdx.x;
-  if (j >= nc) return;
   const uint64_t base = (uint64_t)f * a.max_chunks;
-  ParseState ps = in[base + j];
-  if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
-  LaneBits br;
-  br.p = a.streams + (uint64_t)f * a.stream_stride;
-  br.len = len;
-  br.seek(ps.pos);
-  const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
-  const uint64_t hard = len * 8 + 64;
+  unsigned long long e = 0, last = ~0ull;
+  if (j < nc) {
+    e = j == 0 ? 0ull : a.entry[base + j];
+    last = a.last[base + j];
+  }
+  const bool need = j < nc && (last == ~0ull || (last & PS_MASK) != e);
+  if (!__syncthreads_or(need)) return;
+  const DecTables* T = reinterpret_cast<const DecTables*>(a.tables) + f;
+  load_lut(S, T);
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6;
+  if (jb * 256u + wave * 64u >= nc) return;
+  uint32_t* wring = ring + wave * 64u * RING_STRIDE;
+  const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
+  const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const bool check = last != ~0ull;
+  const uint32_t nvalid_old = (uint32_t)(last >> 56);
+  const unsigned long long begin = D + (unsigned long long)j * DEC_CHUNK_BITS;
+  const unsigned long long end = begin + DEC_CHUNK_BITS;
+  const unsigned long long hard = len * 8 + 64;
   const uint64_t N = (uint64_t)a.W * a.H;
+  unsigned long long* ck = a.ck + (uint64_t)f * DEC_N_CK * a.max_chunks + j;
+  Lane L;
+  lane_seek(L, D + (e & ((1ull << 40) - 1)));
+  uint32_t g = (uint32_t)(e >> 40) & 15u, dk = (uint32_t)(e >> 44) & 127u;
   uint64_t px = 0;
-  while (ps.pos < end && ps.pos < hard && px <= N) parse_step(br, T, ps, px);
-  // pixels this chunk produces from its current entry: exact once entries are final
+  uint32_t k = 0;
+  unsigned long long next_ck = begin + DEC_CK_BITS;
+  unsigned long long ck_old = (check && nvalid_old > 0) ? ck[0] : ~0ull;
+  bool active = need, synced = false;
+  while (__any(active)) {
+    ring_fill(wring, p, len, al16, L);
+    while (active && L.ok) {
+      if (L.pos >= end || L.pos >= hard || px > N) { active = false; break; }
+      gstep(ring_symbol(L, my, S, T, g), g, dk, px);
+      if (L.pos >= next_ck) {
+        const uint32_t cur = (uint32_t)(L.pos - begin) | (g << 16) | (dk << 20);
+        if (check && k < nvalid_old && (uint32_t)ck_old == cur) { synced = true; active = false; break; }
+        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)min(px, (uint64_t)0xFFFFFFFFu) << 32);
+        ++k;
+        next_ck = k < DEC_N_CK ? next_ck + DEC_CK_BITS : ~0ull;
+        ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
+      }
+    }
+  }
+  if (!need) return;
+  if (synced) {
+    // from checkpoint k on this parse equals the previous one, shifted by delta pixels
+    const uint32_t delta = (uint32_t)px - (uint32_t)(ck_old >> 32);
+    a.chunk_px[base + j] = a.chunk_px[base + j] + (uint64_t)(int64_t)(int32_t)delta;
+    for (uint32_t kk = k; kk < nvalid_old; ++kk) {
+      unsigned long long& c = ck[(uint64_t)kk * a.max_chunks];
+      c = (c & 0xFFFFFFFFull) | ((unsigned long long)((uint32_t)(c >> 32) + delta) << 32);
+    }
+    a.last[base + j] = e | ((unsigned long long)nvalid_old << 56);
+    return;
+  }
   a.chunk_px[base + j] = px;
+  a.last[base + j] = e | ((unsigned long long)k << 56);
   if (j + 1 < nc) {
-    const ParseState old = in[base + j + 1];
-    out[base + j + 1] = ps;
-    if (!state_eq(old, ps)) atomicOr(changed, 1u);
+    const unsigned long long x = ps_pack(L.pos - D, g, dk);
+    if (a.entry[base + j + 1] != x) {
+      a.entry[base + j + 1] = x;
+      atomicOr(changed, 1u);
+    }
   }
-  if (j == 0) out[base] = in[base];
-}
-
-// ---------------------------------------------------------------------------
-// D2: pixels per chunk (entries final).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dec_count(DecArgs a, const ParseState* entry) {
-  __shared__ DecTables T;
-  const uint32_t f = blockIdx.x / a.chunk_blocks;
-  const uint32_t jb = blockIdx.x % a.chunk_blocks;
-  if (a.status[f] != 0) return;
-  const uint64_t len = a.stream_len[f];
-  const uint64_t D = a.data_start[f];
-  const uint32_t nc = n_chunks(len, D);
-  if (jb * 256u >= nc) return;
-  load_tables(T, reinterpret_cast<const DecTables*>(a.tables) + f);
-  __syncthreads();
-  const uint32_t j = jb * 256u + threadIdx.x;
-  if (j >= nc) return;
-  const uint64_t base = (uint64_t)f * a.max_chunks;
-  ParseState ps = entry[base + j];
-  if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
-  LaneBits br;
-  br.p = a.streams + (uint64_t)f * a.stream_stride;
-  br.len = len;
-  br.seek(ps.pos);
-  const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
-  const uint64_t hard = len * 8 + 64;
-  uint64_t px = 0;
-  const uint64_t N = (uint64_t)a.W * a.H;
-  while (ps.pos < end && ps.pos < hard && px <= N) parse_step(br, T, ps, px);
-  a.chunk_px[base + j] = px;
 }
 
 // ---------------------------------------------------------------------------
@@ -353,6 +482,8 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
 //   src = floor((L + U) / 2) (L on row 0)      kind AVG: SMALL_DIFF, LUMA2, RGB
 //   src = pixel i - off(refid)                 kind REF: BACK_REF (refid 0..4),
 //                                                        LUMA (refid 5..15)
+// Records of a lane are combined into aligned groups of four and stored with
+// one 16-byte store when the group lies inside the lane's pixel range.
 // ---------------------------------------------------------------------------
 constexpr uint32_t REC_RUN = 0xFFFFFFFFu;
 constexpr uint32_t REC_REF = 1u << 28;
@@ -362,7 +493,6 @@ __host__ __device__ constexpr int ref_px_off(int id) { return id < 5 ? br_px(id)
 __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_t mode, uint32_t s0,
                                            uint32_t s1, uint32_t s2, uint32_t s3, uint32_t* rec) {
   const uint64_t W = a.W;
-  const uint64_t y = q / W;
   switch (mode) {
     case P_BACK_REF:
     case P_LUMA: {
@@ -385,7 +515,7 @@ __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_
       return 0;
     }
     case P_LUMA2: {
-      if (y == 0) return NICE_E_FORMAT;   // position - channels*width underflows (code.rs:583)
+      if (q < W) return NICE_E_FORMAT;   // position - channels*width underflows (code.rs:583)
       const uint32_t g = (s0 - 32u) & 255u;
       *rec = ((s1 - 16u + g) & 255u) | (g << 8) | (((s2 - 16u + g) & 255u) << 16);
       return 0;
@@ -398,8 +528,41 @@ __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_
   }
 }
 
-__global__ __launch_bounds__(256) void dec_emit(DecArgs a, const ParseState* entry) {
-  __shared__ DecTables T;
+struct RecGroup {
+  unsigned long long grp;   // first pixel of the aligned group, ~0: empty
+  uint32_t v0, v1, v2, v3, mask;
+  __device__ __forceinline__ void flush(uint32_t* rec, unsigned long long lo, unsigned long long hi) {
+    if (!mask) return;
+    if (grp >= lo && grp + 4 <= hi) {
+      *reinterpret_cast<uint4*>(rec + grp) = make_uint4(v0, v1, v2, v3);
+    } else {
+      if (mask & 1u) rec[grp] = v0;
+      if (mask & 2u) rec[grp + 1] = v1;
+      if (mask & 4u) rec[grp + 2] = v2;
+      if (mask & 8u) rec[grp + 3] = v3;
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t* rec, unsigned long long lo, unsigned long long cur,
+                                      uint32_t r) {
+    const unsigned long long g4 = cur & ~3ull;
+    if (g4 != grp) {
+      flush(rec, lo, cur);    // every pixel of the old group below cur is this lane's
+      grp = g4;
+      v0 = v1 = v2 = v3 = REC_RUN;
+      mask = 0;
+    }
+    const uint32_t k = (uint32_t)(cur & 3u);
+    v0 = k == 0 ? r : v0;
+    v1 = k == 1 ? r : v1;
+    v2 = k == 2 ? r : v2;
+    v3 = k == 3 ? r : v3;
+    mask |= 1u << k;
+  }
+};
+
+__global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
+  __shared__ LutLds S;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
   const uint32_t f = blockIdx.x / a.chunk_blocks;
   const uint32_t jb = blockIdx.x % a.chunk_blocks;
   if (a.status[f] != 0) return;
@@ -407,76 +570,97 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a, const ParseState* ent
   const uint64_t D = a.data_start[f];
   const uint32_t nc = n_chunks(len, D);
   if (jb * 256u >= nc) return;
-  load_tables(T, reinterpret_cast<const DecTables*>(a.tables) + f);
+  const DecTables* T = reinterpret_cast<const DecTables*>(a.tables) + f;
+  load_lut(S, T);
   __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6;
+  if (jb * 256u + wave * 64u >= nc) return;
   const uint32_t j = jb * 256u + threadIdx.x;
-  if (j >= nc) return;
+  uint32_t* wring = ring + wave * 64u * RING_STRIDE;
+  const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
+  const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   const uint64_t base = (uint64_t)f * a.max_chunks;
   const uint64_t N = (uint64_t)a.W * a.H;
-  uint64_t q = a.chunk_start[base + j];   // pixels accounted before this chunk
-  if (q > N) return;                      // past the image: tail bytes
-  ParseState ps = entry[base + j];
-  if (j == 0) { ps.pos = D; ps.g = 0; ps.dk = 0; ps.acc = 0; }
-  LaneBits src;
-  src.p = a.streams + (uint64_t)f * a.stream_stride;
-  src.len = len;
-  src.seek(ps.pos);
-  const uint64_t end = D + (uint64_t)(j + 1) * DEC_CHUNK_BITS;
-  const uint64_t hard = len * 8 + 64;
-  uint32_t* rec = a.recs + (uint64_t)f * N;
+  unsigned long long q = 0, e = 0;
+  bool active = j < nc;
+  if (active) {
+    q = a.chunk_start[base + j];   // pixels accounted before this chunk
+    e = j == 0 ? 0ull : a.entry[base + j];
+    if (q > N) active = false;     // past the image: tail bytes
+  }
+  const unsigned long long q0 = q;
+  const unsigned long long end = D + (unsigned long long)(j + 1) * DEC_CHUNK_BITS;
+  const unsigned long long hard = len * 8 + 64;
+  uint32_t* rec = a.recs + (uint64_t)f * a.rec_stride;
   const bool strict = (a.flags & NICE_DEC_STRICT_REFERENCE) != 0;
+  Lane L;
+  lane_seek(L, D + (e & ((1ull << 40) - 1)));
+  uint32_t g = (uint32_t)(e >> 40) & 15u, dk = (uint32_t)(e >> 44) & 127u;
   // the pixel whose payload straddles our entry belongs to the previous chunk
-  while (ps.g != 0 && ps.pos < hard) { uint64_t px = 0; parse_step(src, T, ps, px); }
-  bool closed = (q == N);                 // a run completed exactly at N earlier
+  bool straddle = true;
+  bool closed = (q == N);          // a run completed exactly at N earlier
   uint32_t mode = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  uint64_t cur = 0;
-  while (ps.pos < hard) {
-    if (ps.g == 0) {
-      if (q == N && (ps.dk == 0 || closed)) {
-        // every pixel is accounted for; the reference still reads one more prefix
-        // (code.rs:660): a run digit there makes it copy past its buffer
-        if (strict) {
-          uint64_t px = 0;
-          const uint32_t sym = parse_step(src, T, ps, px);
-          if (sym >= (uint32_t)P_RUN1) set_status(&a.status[f], NICE_E_FORMAT);
-        }
-        return;
-      }
-      if (ps.pos >= end) return;          // next chunk continues from here
-    }
-    const uint32_t g0 = ps.g, dk0 = ps.dk;
-    uint64_t px = 0;
-    const uint32_t sym = parse_step(src, T, ps, px);
-    if (g0 == 0) {
-      if (sym >= (uint32_t)P_RUN1) {      // run digit
-        if (q == N && dk0 == 0) {         // a digit right after the last pixel
-          if (strict) set_status(&a.status[f], NICE_E_FORMAT);
-          return;
-        }
-        q += px;
-        if (q > N) { set_status(&a.status[f], NICE_E_FORMAT); return; }
-        if (q == N) closed = true;
+  unsigned long long cur = 0;
+  int err = 0;
+  RecGroup G{~0ull, REC_RUN, REC_RUN, REC_RUN, REC_RUN, 0u};
+  while (__any(active)) {
+    ring_fill(wring, p, len, al16, L);
+    while (active && L.ok) {
+      if (L.pos >= hard) { active = false; break; }
+      uint64_t px = 0;
+      if (straddle) {
+        if (g == 0) { straddle = false; continue; }
+        gstep(ring_symbol(L, my, S, T, g), g, dk, px);
         continue;
       }
-      closed = false;
-      mode = sym;
-      cur = q;
-      q += 1;
-      continue;
-    }
-    switch (g0) {
-      case 1: case 2: case 5: case 9: case 10: s0 = sym; break;
-      case 3: case 6: case 11: s1 = sym; break;
-      case 4: case 7: case 12: s2 = sym; break;
-      default: s3 = sym; break;
-    }
-    if (ps.g == 0) {                       // payload complete
-      uint32_t r;
-      const int e = make_record(a, cur, mode, s0, s1, s2, s3, &r);
-      if (e) { set_status(&a.status[f], e); return; }
-      rec[cur] = r;
+      if (g == 0) {
+        if (q == N && (dk == 0 || closed)) {
+          // every pixel is accounted for; the reference still reads one more prefix
+          // (code.rs:660): a run digit there makes it copy past its buffer
+          if (strict) {
+            const uint32_t sym = gstep(ring_symbol(L, my, S, T, g), g, dk, px);
+            if (sym >= (uint32_t)P_RUN1) err = NICE_E_FORMAT;
+          }
+          active = false;
+          break;
+        }
+        if (L.pos >= end) { active = false; break; }   // next chunk continues from here
+      }
+      const uint32_t g0 = g, dk0 = dk;
+      const uint32_t sym = gstep(ring_symbol(L, my, S, T, g), g, dk, px);
+      if (g0 == 0) {
+        if (sym >= (uint32_t)P_RUN1) {      // run digit
+          if (q == N && dk0 == 0) {         // a digit right after the last pixel
+            if (strict) err = NICE_E_FORMAT;
+            active = false;
+            break;
+          }
+          q += px;
+          if (q > N) { err = NICE_E_FORMAT; active = false; break; }
+          if (q == N) closed = true;
+          continue;
+        }
+        closed = false;
+        mode = sym;
+        cur = q;
+        q += 1;
+        continue;
+      }
+      s0 = (g0 == 1 || g0 == 2 || g0 == 5 || g0 == 9 || g0 == 10) ? sym : s0;
+      s1 = (g0 == 3 || g0 == 6 || g0 == 11) ? sym : s1;
+      s2 = (g0 == 4 || g0 == 7 || g0 == 12) ? sym : s2;
+      s3 = (g0 == 8) ? sym : s3;
+      if (g == 0) {                          // payload complete
+        uint32_t r;
+        const int e2 = make_record(a, cur, mode, s0, s1, s2, s3, &r);
+        if (e2) { err = e2; active = false; break; }
+        G.put(rec, q0, cur, r);
+      }
     }
   }
+  G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
+  if (err) set_status(&a.status[f], err);
 }
 
 // ---------------------------------------------------------------------------
@@ -611,9 +795,8 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   }
   if (lane == 0) L.err = 0;
   __syncthreads();
-  const uint64_t N = (uint64_t)W * H;
   const uint32_t S = a.seg, nseg = a.nseg;
-  const uint32_t* recs = a.recs + (uint64_t)f * N;
+  const uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride;
   uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
   const uint32_t OC = a.out_channels;
   const uint8_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 255 : 0;

@@ -91,7 +91,6 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
   __shared__ TileWin tw;
   __shared__ uint32_t hist[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
-  __shared__ uint32_t tile_min, tile_max;
 
   const uint64_t total_tiles = (uint64_t)a.n_frames * a.tiles_per_frame;
   const uint64_t t_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
@@ -120,7 +119,6 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
     __syncthreads();
     stage_tile(tw, frame, start, N, a.W, a.C);
-    if (threadIdx.x == 0) { tile_min = NONE; tile_max = NONE; }
     __syncthreads();
 
     // coded flags -> bitmask

@@ -51,12 +51,9 @@ __global__ void enc_serial(EncArgs a);
 namespace nice {
 
 constexpr uint32_t DEC_CHUNK_BITS = 2048;   // speculative-parse slice
+constexpr uint32_t DEC_CK_BITS = 128;       // sync checkpoint spacing inside a chunk
+constexpr uint32_t DEC_N_CK = DEC_CHUNK_BITS / DEC_CK_BITS - 1;
 constexpr int DEC_MAX_SEGS = 64;            // one lane per row segment
-
-struct SegBound {
-  unsigned long long pos;   // bit position of the next coded pixel's prefix
-  unsigned long long run;   // run pixels (copies of the left neighbour) before it
-};
 
 struct DecArgs {
   const uint8_t* streams;
@@ -71,22 +68,24 @@ struct DecArgs {
   void* tables;                       // n_frames DecTables
   unsigned long long* data_start;     // n_frames
   uint32_t max_chunks, chunk_blocks;  // per frame
+  unsigned long long* entry;          // n_frames * max_chunks packed entry states
+  unsigned long long* last;           // n_frames * max_chunks entry of the last parse
+  unsigned long long* ck;             // n_frames * DEC_N_CK * max_chunks checkpoints
   unsigned long long* chunk_px;       // n_frames * max_chunks
   unsigned long long* chunk_start;    // n_frames * max_chunks
-  uint32_t* recs;                     // n_frames * W * H per-pixel records
+  uint32_t* recs;                     // n_frames * rec_stride per-pixel records
+  uint64_t rec_stride;                // W * H rounded up to 4 (16-byte aligned frames)
   uint32_t seg, nseg;
   uint32_t rows_in_lds;               // 1: row ring in LDS, 0: in rowbuf
   uint32_t* rowbuf;                   // n_frames * R * W (when not in LDS)
   unsigned long long* stats;          // optional diagnostics (NICE_DEC_STATS=1), else null
 };
 
-struct ParseState;
 __global__ void dec_tables(DecArgs a);
-__global__ void dec_init_entries(DecArgs a, ParseState* e);
-__global__ void dec_sync(DecArgs a, const ParseState* in, ParseState* out, uint32_t* changed);
-__global__ void dec_count(DecArgs a, const ParseState* entry);
+__global__ void dec_init_entries(DecArgs a);
+__global__ void dec_sync(DecArgs a, uint32_t* changed);
 __global__ void dec_scan(DecArgs a);
-__global__ void dec_emit(DecArgs a, const ParseState* entry);
+__global__ void dec_emit(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);
 
 }  // namespace nice

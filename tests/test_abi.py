@@ -63,10 +63,13 @@ def test_cpp_mirror_compiles(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cpp_mirror_roundtrip():
+def test_cpp_mirror_roundtrip(tmp_path, O):
     import subprocess
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "examples"), "roundtrip"])
-    out = subprocess.run([os.path.join(ROOT, "examples", "roundtrip"), "1283", "719"],
+    path = str(tmp_path / "s.nice")
+    out = subprocess.run([os.path.join(ROOT, "examples", "roundtrip"), "1283", "719", path],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.startswith("ok")
+    # the example's frame is NICE-SYN-v1 seed 1: its stream is the oracle's
+    assert open(path, "rb").read() == O.encode(O.gen_syn_v1(1283, 719, 4, 1), 1283, 719, 4)
