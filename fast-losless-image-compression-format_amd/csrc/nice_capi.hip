@@ -408,7 +408,14 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   const uint32_t max_chunks =
       max_len * 8 > D ? (uint32_t)((max_len * 8 - D + DEC_CHUNK_BITS - 1) / DEC_CHUNK_BITS) : 1;
   const RecGeom g = rec_geom(w);
-  const size_t rowbuf = g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4;
+  // multi-wave row kernel for 64 <= W <= 16384 (one lane per 16-pixel segment),
+  // single-wave kernel otherwise
+  const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
+  const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
+  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * w) * 4;
+  const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
+  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * w * 4)
+                                 : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
   DecLayout L = dec_layout(n_frames, max_chunks, N, rowbuf);
   int rc = ctx->dec.grow(L.total);
   if (rc) return rc;
@@ -469,7 +476,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
   tm.begin(NICE_PH_DEC_BOUNDS, st);
-  NICE_HIP(hipMemsetAsync(a.recs, 0xFF, (size_t)n_frames * a.rec_stride * 4, st));   // REC_RUN fill
+  NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
   hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a);
   tm.end(st);
   if (g.lds > 64 * 1024)
@@ -477,22 +484,33 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
   static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
   unsigned long long* dstats = nullptr;
-  if (want_stats && hipMalloc(&dstats, 128) == hipSuccess) {
-    (void)hipMemsetAsync(dstats, 0, 128, st);
+  if (want_stats && hipMalloc(&dstats, 256) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 256, st);
     a.stats = dstats;
   }
   tm.begin(NICE_PH_DEC_RECON, st);
-  hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
+  if (use_rows && rows_in_lds) {
+    if (rows_lds > 64 * 1024)
+      NICE_HIP(hipFuncSetAttribute((const void*)dec_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)rows_lds));
+    hipLaunchKernelGGL(dec_rows, dim3(n_frames), dim3(rows_thr), rows_lds, st, a);
+  } else if (use_rows) {
+    hipLaunchKernelGGL(dec_rows_wide, dim3(n_frames), dim3(rows_thr), ((size_t)rows_thr * 7 + 8) * 4, st, a);
+  } else {
+    hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, a);
+  }
   tm.end(st);
   if (dstats) {
-    unsigned long long h[16] = {0};
-    (void)hipMemcpyAsync(h, dstats, 128, hipMemcpyDeviceToHost, st);
+    unsigned long long h[32] = {0};
+    (void)hipMemcpyAsync(h, dstats, 256, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
             "[nice dec stats] rows=%llu unconverged_segs=%llu tail_unknown_segs=%llu "
             "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
             "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
             h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
+    fprintf(stderr, "[nice dec stats] fix-up rounds per row: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5:%llu 6+:%llu\n",
+            h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
     (void)hipFree(dstats);
   }
   NICE_HIP(hipGetLastError());

@@ -485,10 +485,37 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
 // Records of a lane are combined into aligned groups of four and stored with
 // one 16-byte store when the group lies inside the lane's pixel range.
 // ---------------------------------------------------------------------------
-constexpr uint32_t REC_RUN = 0xFFFFFFFFu;
-constexpr uint32_t REC_REF = 1u << 28;
-__host__ __device__ constexpr int ref_rows(int id) { return id < 5 ? br_rows(id) : lr_rows(id - 5); }
-__host__ __device__ constexpr int ref_px_off(int id) { return id < 5 ? br_px(id) : lr_px(id - 5); }
+// Record: bits 0..23 the additive constant c (R | G << 8 | B << 16), bits
+// 24..27 the source class: 0 = AVG, 1..3 = the pixel 1..3 back in raster order
+// (a run pixel is class 1 with c = 0), 4..13 = a pixel in a row above, at
+// (rows back, pixels back) = cls_rows / cls_px.
+constexpr uint32_t REC_RUN = 1u << 24;
+__host__ __device__ constexpr int cls_rows(int c) {
+  return c < 4 ? 0 : c == 4 ? 1 : c == 5 ? 1 : c == 6 ? 2 : c == 7 ? 1 : c <= 10 ? 3 : c == 11 ? 1 : c <= 13 ? 3 : 0;
+}
+__host__ __device__ constexpr int cls_px(int c) {
+  return c < 4 ? c : c == 4 ? 0 : c == 5 ? -1 : c == 6 ? 0 : c == 7 ? -3 : c == 8 ? -1 : c == 9 ? 0
+       : c == 10 ? 1 : c == 11 ? 3 : c == 12 ? 3 : c == 13 ? -3 : 0;
+}
+// reference id (back refs 0..4, luma refs 5..15) -> class
+__host__ __device__ constexpr int id_cls(int id) {
+  return id == 0 ? 1 : id == 1 ? 4 : id == 2 ? 5 : id == 3 ? 2 : id == 4 ? 6
+       : id == 5 ? 1 : id == 6 ? 4 : id == 7 ? 5 : id == 8 ? 7 : id == 9 ? 3 : id == 10 ? 8
+       : id == 11 ? 9 : id == 12 ? 10 : id == 13 ? 11 : id == 14 ? 12 : 13;
+}
+__host__ __device__ constexpr bool cls_table_ok() {
+  for (int id = 0; id < 16; ++id) {
+    const int rows = id < 5 ? br_rows(id) : lr_rows(id - 5), px = id < 5 ? br_px(id) : lr_px(id - 5);
+    if (cls_rows(id_cls(id)) != rows || cls_px(id_cls(id)) != px) return false;
+  }
+  return true;
+}
+static_assert(cls_table_ok(), "reference offsets (code.rs:141-145) map onto the record classes");
+constexpr unsigned long long ID_CLS_PACK = [] {
+  unsigned long long v = 0;
+  for (int id = 0; id < 16; ++id) v |= (unsigned long long)id_cls(id) << (4 * id);
+  return v;
+}();
 
 __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_t mode, uint32_t s0,
                                            uint32_t s1, uint32_t s2, uint32_t s3, uint32_t* rec) {
@@ -498,7 +525,8 @@ __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_
     case P_LUMA: {
       const uint32_t id = mode == P_BACK_REF ? s0 : 5u + s0;
       if ((mode == P_BACK_REF && s0 >= 5) || (mode == P_LUMA && s0 >= 11)) return NICE_E_FORMAT;
-      const int64_t off = (int64_t)ref_rows((int)id) * (int64_t)W + ref_px_off((int)id);
+      const uint32_t cls = (uint32_t)(ID_CLS_PACK >> (4 * id)) & 15u;
+      const int64_t off = (int64_t)cls_rows((int)cls) * (int64_t)W + cls_px((int)cls);
       // usize wrap (W < 3) or underflow before the image: the reference panics
       if (off < 0 || (int64_t)q < off) return NICE_E_FORMAT;
       uint32_t c = 0;
@@ -506,7 +534,7 @@ __device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_
         const uint32_t g = (s1 - 32u) & 255u;
         c = ((s2 - 16u + g) & 255u) | (g << 8) | (((s3 - 16u + g) & 255u) << 16);
       }
-      *rec = REC_REF | (id << 24) | c;
+      *rec = (cls << 24) | c;
       return 0;
     }
     case P_SMALL_DIFF: {
@@ -669,7 +697,7 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
 struct RecLds {
   uint32_t y4tail[4];
   int32_t ref_k[16], ref_d[16];
-  int32_t ref_off32[16];   // k*W + d, clamped to [0, 4] (only 0..3 are special)
+  int32_t ref_off32[16];   // k*W + d per record class, clamped to [0, 4] (only 0..3 are special)
   int32_t err;
   uint32_t pad[3];
 };
@@ -732,9 +760,8 @@ __device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, co
   for (uint32_t x = x0; x < x_stop; ++x) {
     const uint32_t r = recs[x];
     const uint32_t u = up[x];
-    const bool run = r == REC_RUN;
-    const bool ref = !run && (r & REC_REF);
-    const uint32_t c = run ? 0u : spread3(r);
+    const bool ref = (r >> 24) != 0;   // run pixels are class 1 (the pixel before) with c = 0
+    const uint32_t c = spread3(r & 0xFFFFFFu);
     // reference value (kind REF): recent pixels or a pixel of the ring
     const int id = (int)((r >> 24) & 15u);
     const int off = (int)L.ref_off32[id];
@@ -760,7 +787,7 @@ __device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, co
     src = ref ? src : r0;
     const IvS va = ivs_avg(r0, u, c);
     const IvS vr = ivs_add(src, c);
-    const bool avg = !run && !ref && has_up;
+    const bool avg = !ref && has_up;
     const IvS v{avg ? va.lo : vr.lo, avg ? va.len : vr.len};
     row[x] = v.lo;
     last_unknown = v.len ? (int)(x - x0) : last_unknown;
@@ -788,9 +815,9 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   const int lane = threadIdx.x;
   if (a.status[f] != 0) return;
   if (lane < 16) {
-    L.ref_k[lane] = ref_rows(lane);
-    L.ref_d[lane] = ref_px_off(lane);
-    const int64_t off = (int64_t)ref_rows(lane) * W + ref_px_off(lane);
+    L.ref_k[lane] = cls_rows(lane);
+    L.ref_d[lane] = cls_px(lane);
+    const int64_t off = (int64_t)cls_rows(lane) * W + cls_px(lane);
     L.ref_off32[lane] = (int32_t)(off < 0 ? 4 : off > 4 ? 4 : off);
   }
   if (lane == 0) L.err = 0;
@@ -890,6 +917,314 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   }
   if (lane == 0 && L.err) set_status(&a.status[f], L.err);
 }
+
+// ---------------------------------------------------------------------------
+// D5b: multi-wave reconstruction (64 <= W <= 16384).  One block per frame,
+// one lane per 16-pixel row segment (up to 1024 lanes).  A lane keeps its
+// segment of the row above and of the current row in registers (the segment
+// loop is unrolled), so the left-to-right recurrence touches no memory:
+//   pre-pass  records (prefetched one row ahead) -> per-pixel kind and
+//             constant; references into rows above read a ring of the last
+//             four rows (LDS when it fits, else global)
+//   spec      from the exact entry (lane 0) or an unknown one (others), as
+//             per-channel cyclic intervals that collapse within a few pixels
+//   fix-up    rounds across the block: a lane whose left neighbour's last
+//             three pixels are exact recomputes its unknown prefix exactly;
+//             the others refine theirs from the neighbour's current intervals
+//             (sound, so anything that collapses is final)
+//   emit      pixels to the ring and the caller's raster
+// ---------------------------------------------------------------------------
+constexpr int ROWS_SEG = 16;
+constexpr uint32_t ROWS_RING = 4;   // rows y-4 .. y-1 while row y is built
+
+constexpr uint32_t CLS_ROWS_PACK = [] {
+  uint32_t v = 0;
+  for (int c = 0; c < 16; ++c) v |= (uint32_t)cls_rows(c) << (2 * c);
+  return v;
+}();
+constexpr unsigned long long CLS_PX_PACK = [] {
+  unsigned long long v = 0;
+  for (int c = 0; c < 16; ++c) v |= (unsigned long long)(cls_px(c) + 3) << (3 * c);
+  return v;
+}();
+
+// Per-pixel word: spread constant c in the field bits, the kind as one-hot
+// flags in the guard bits -- W_L1/W_L2/W_L3: c plus the pixel 1..3 back;
+// W_AVG: c plus floor((left + up) / 2); W_CUR: c plus one of pixels 0..2 of the
+// current row (index in bits 8..9), unknown until lane 0 has them; none: the
+// constant itself (a reference into a row above, already added).
+constexpr uint32_t W_L1 = 1u << 28, W_AVG = 1u << 31, W_CUR = 1u << 18;   // W_L2, W_L3: bits 29, 30
+__device__ __forceinline__ uint32_t wmask(uint32_t w, int bit) {
+  return (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1);   // 0 or ~0
+}
+// One pixel: kinds are selected with masks (no control flow, no SGPR masks).
+__device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uint32_t wp) {
+  const uint32_t c = wp & SP_K;
+  const IvS va = ivs_avg(l1, u, c);
+  const uint32_t m1 = wmask(wp, 28), m2 = wmask(wp, 29), m3 = wmask(wp, 30);
+  const uint32_t ma = wmask(wp, 31), mc = wmask(wp, 18);
+  const uint32_t slo = (l1.lo & m1) | (l2.lo & m2) | (l3.lo & m3);
+  const uint32_t slen = (l1.len & m1) | (l2.len & m2) | (l3.len & m3) | (SP_K & mc);
+  const uint32_t rlo = (slo + c) & SP_K;
+  return IvS{(va.lo & ma) | (rlo & ~ma), (va.len & ma) | (slen & ~ma)};
+}
+
+// Speculative pass over the whole segment; returns the last unknown index.
+template <int S>
+__device__ __forceinline__ int rows_spec(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                         const uint32_t (&prev)[S], int nvalid) {
+  int lu = -1;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const IvS l1 = p >= 1 ? v[p - 1] : r0;
+    const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
+    const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
+    v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
+    lu = (p < nvalid && v[p].len) ? p : lu;
+  }
+  return lu;
+}
+
+// Recomputes pixels 0..lu (lanes with `go`), keeping the others (already
+// exact); returns the new last unknown index.  Stops once no lane of the wave
+// has work left.
+template <int S>
+__device__ __forceinline__ int rows_chain(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                          const uint32_t (&prev)[S], int nvalid, int lu, bool go) {
+  int nlu = -1;
+  const int upto = go ? lu : -1;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    if (!__any(p <= upto)) break;
+    const IvS l1 = p >= 1 ? v[p - 1] : r0;
+    const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
+    const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
+    const IvS n = rows_step(l1, l2, l3, prev[p], w[p]);
+    const bool upd = p <= upto;
+    v[p].lo = upd ? n.lo : v[p].lo;
+    v[p].len = upd ? n.len : v[p].len;
+    nlu = (upd && p < nvalid && n.len) ? p : nlu;
+  }
+  return go ? nlu : lu;
+}
+
+// Block barrier; with the ring in LDS only LDS traffic is ordered, so global
+// stores (the raster) and the record prefetch stay in flight across it.
+template <bool LDS_RING>
+__device__ __forceinline__ void rows_barrier() {
+  if constexpr (LDS_RING) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int MAXT, bool LDS_RING>
+__device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
+  constexpr int S = ROWS_SEG;
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  const uint32_t nthr = blockDim.x;
+  const uint32_t W = a.W, H = a.H;
+  uint32_t* tails = sm;                 // nthr x {lo, len} x 3 (pixels S-1, S-2, S-3)
+  uint32_t* flags = tails + nthr * 6;   // nthr: last three pixels exact
+  uint32_t* head3 = flags + nthr;       // pixels 0..2 of the current row
+  uint32_t* pend = head3 + 4;           // 2 round flags
+  int* err = reinterpret_cast<int*>(pend + 2);
+  const uint32_t f = blockIdx.x;
+  uint32_t* ring = LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * W);
+  if (a.status[f] != 0) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nseg = (W + S - 1) / S;
+  const bool active = lane < nseg;
+  const uint32_t x0 = lane * S;
+  const int nvalid = active ? (int)min((uint32_t)S, W - x0) : 0;
+  const uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride;
+  uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
+  const uint32_t OC = a.out_channels;
+  const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const bool vec_rec = (W & 3u) == 0 && nvalid == S;
+  const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) || (OC == 3 && (W & 15u) == 0 && nvalid == S);
+  if (lane == 0) *err = 0;
+  uint32_t prev[S], rn[S];
+#pragma unroll
+  for (int p = 0; p < S; ++p) prev[p] = 0;
+  auto load_recs = [&](uint32_t y) {
+    const uint32_t* rrow = recs + (uint64_t)y * W + x0;
+    if (vec_rec) {
+#pragma unroll
+      for (int q = 0; q < S / 4; ++q) {
+        const uint4 t = reinterpret_cast<const uint4*>(rrow)[q];
+        rn[4 * q] = t.x; rn[4 * q + 1] = t.y; rn[4 * q + 2] = t.z; rn[4 * q + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = p < nvalid ? rrow[p] : REC_RUN;
+    }
+  };
+  if (H > 0) load_recs(0);
+  __syncthreads();
+  unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0, n_fix = 0;
+  for (uint32_t y = 0; y < H; ++y) {
+    const unsigned long long c0 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    // ---- pre-pass: records -> per-pixel words
+    uint32_t w[S];
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+      const uint32_t x = x0 + p;
+      const uint32_t r = rn[p];
+      const uint32_t cls = r >> 24;                          // 0..13
+      const uint32_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
+      const int dx = (int)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;
+      int tx = (int)x - dx;
+      const int wl = tx < 0, wr = tx >= (int)W;
+      tx += wl ? (int)W : (wr ? -(int)W : 0);
+      const uint32_t back = rows + wl - wr;                  // rows above (0: current row)
+      const bool up = cls >= 4;
+      const bool cur = up && back == 0;
+      // unconditional LDS read (a harmless in-range address for other classes)
+      const uint32_t o = ring[(size_t)((y - back) & (ROWS_RING - 1)) * W + (uint32_t)min(max(tx, 0), (int)W - 1)];
+      const uint32_t c = spread3(r & 0xFFFFFFu);
+      const uint32_t kb = cls == 0 ? (y == 0 ? W_L1 : W_AVG)
+                        : cls < 4 ? (W_L1 << (cls - 1u)) : (cur ? W_CUR : 0u);
+      w[p] = kb | ((up && !cur) ? ((o + c) & SP_K) : c) | (cur ? ((uint32_t)tx << 8) : 0u);
+    }
+    // ---- entry: lane 0 exact (previous row's last pixels; 0 before pixel 0)
+    IvS r0{0u, SP_K}, r1{0u, SP_K}, r2{0u, SP_K};
+    if (lane == 0) {
+      if (y == 0) {
+        r0 = r1 = r2 = ivs_exact(0u);
+      } else {
+        const uint32_t* pr = ring + (size_t)((y - 1) & (ROWS_RING - 1)) * W;
+        r0 = ivs_exact(pr[W - 1]);
+        r1 = ivs_exact(pr[W - 2]);
+        r2 = ivs_exact(pr[W - 3]);
+      }
+    }
+    if (y + 1 < H) load_recs(y + 1);   // in flight during this row
+    const unsigned long long c1 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    // ---- speculative pass
+    IvS v[S];
+    int lu = rows_spec<S>(v, r0, r1, r2, w, prev, nvalid);
+    if (active) {
+      uint32_t* t = tails + lane * 6;
+      t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
+      t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
+      t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
+      flags[lane] = (lu < S - 3) ? 1u : 0u;
+    }
+    if (lane == 0) { head3[0] = v[0].lo; head3[1] = v[1].lo; head3[2] = v[2].lo; pend[0] = 0; pend[1] = 0; }
+    bool fin = !active || lu < 0;
+    if (a.stats && active && lu >= 0) {
+      atomicAdd(&a.stats[1], 1ull);
+      atomicAdd(&a.stats[3], (unsigned long long)(lu + 1));
+      if (lu >= S - 3) atomicAdd(&a.stats[2], 1ull);
+    }
+    rows_barrier<LDS_RING>();
+    const unsigned long long c2 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long nfix0 = n_fix;
+    // ---- fix-up rounds
+    bool cur_done = false;
+    for (uint32_t rd = 0;; ++rd) {
+      if (!fin) atomicOr(&pend[rd & 1u], 1u);
+      rows_barrier<LDS_RING>();
+      if (pend[rd & 1u] == 0) break;
+      ++n_fix;
+      if (lane == 0) pend[(rd + 1) & 1u] = 0;
+      if (!cur_done) {   // pixels 0..2 of the row are exact now (lane 0)
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          if (w[p] & W_CUR) w[p] = (head3[(w[p] >> 8) & 3u] + (w[p] & SP_K)) & SP_K;
+        }
+        cur_done = true;
+      }
+      bool exact_in = false;
+      if (!fin && lane > 0) {
+        const uint32_t* t = tails + (lane - 1) * 6;
+        r0 = IvS{t[0], t[1]}; r1 = IvS{t[2], t[3]}; r2 = IvS{t[4], t[5]};
+        exact_in = flags[lane - 1] != 0;
+      }
+      rows_barrier<LDS_RING>();
+      lu = rows_chain<S>(v, r0, r1, r2, w, prev, nvalid, lu, !fin);
+      if (!fin) {
+        if (exact_in && lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
+        uint32_t* t = tails + lane * 6;
+        t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
+        t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
+        t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
+        flags[lane] = (lu < S - 3) ? 1u : 0u;
+        fin = lu < 0 || exact_in;
+      }
+    }
+    if (a.stats && lane == 0) {
+      const unsigned long long r = n_fix - nfix0;
+      atomicAdd(&a.stats[9 + (r >= 6 ? 6 : r)], 1ull);
+    }
+    if (*err) break;
+    const unsigned long long c3 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    // ---- emit: ring row y (its slot held row y-4, no longer referenced) and the raster
+    if (active) {
+      uint32_t* rr = ring + (size_t)(y & (ROWS_RING - 1)) * W + x0;
+      const uint64_t pix = (uint64_t)y * W + x0;
+#pragma unroll
+      for (int p = 0; p < S; ++p)
+        if (p < nvalid) rr[p] = v[p].lo;
+      if (vec_out && OC == 4) {
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q)
+          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
+                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+      } else if (vec_out) {
+        uint32_t b[3 * S / 4];
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) {
+          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
+          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
+          b[3 * q] = u0 | (u1 << 24);
+          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
+          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+        }
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
+#pragma unroll
+        for (int q = 0; q < 3 * S / 16; ++q) o[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+      } else if (OC == 4) {
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(outp + pix * 4);
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+          if (p < nvalid) o32[p] = unspread3(v[p].lo) | alpha;
+      } else {
+        uint8_t* o8 = outp + pix * 3;
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          if (p < nvalid) {
+            const uint32_t u = unspread3(v[p].lo);
+            o8[3 * p] = (uint8_t)u; o8[3 * p + 1] = (uint8_t)(u >> 8); o8[3 * p + 2] = (uint8_t)(u >> 16);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < S; ++p) { prev[p] = v[p].lo; }
+    rows_barrier<LDS_RING>();
+    if (a.stats) {
+      const unsigned long long c4 = __builtin_amdgcn_s_memtime();
+      t_a += c1 - c0; t_b += c2 - c1; t_c += c3 - c2; t_d += c4 - c3;
+    }
+  }
+  if (a.stats && lane == 0) {
+    atomicAdd(&a.stats[0], (unsigned long long)H);
+    atomicAdd(&a.stats[4], n_fix);
+    atomicAdd(&a.stats[5], t_a); atomicAdd(&a.stats[6], t_b);
+    atomicAdd(&a.stats[7], t_c); atomicAdd(&a.stats[8], t_d);
+  }
+  if (lane == 0 && *err) set_status(&a.status[f], *err);
+}
+
+// Ring in LDS (4 rows fit next to the block's tails) or in global memory.
+__global__ __launch_bounds__(512) void dec_rows(DecArgs a) { dec_rows_body<512, true>(a); }
+__global__ __launch_bounds__(1024) void dec_rows_wide(DecArgs a) { dec_rows_body<1024, false>(a); }
 
 __global__ __launch_bounds__(64) void dec_reconstruct(DecArgs a) {
   if (a.rows_in_lds) dec_reconstruct_body<true>(a);

@@ -87,5 +87,7 @@ __global__ void dec_sync(DecArgs a, uint32_t* changed);
 __global__ void dec_scan(DecArgs a);
 __global__ void dec_emit(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);
+__global__ void dec_rows(DecArgs a);
+__global__ void dec_rows_wide(DecArgs a);
 
 }  // namespace nice
