@@ -175,8 +175,8 @@ def main():
     L.nice_ctx_set_timing(ctx.ptr, 1)
     barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
     elapsed = timed_region(step, args.steps, torch.cuda.synchronize, barrier)
-    ms = (ctypes.c_double * 12)()
-    cnt = (ctypes.c_uint32 * 12)()
+    ms = (ctypes.c_double * 32)()
+    cnt = (ctypes.c_uint32 * 32)()
     L.nice_ctx_read_timing(ctx.ptr, ms, cnt)
     L.nice_ctx_set_timing(ctx.ptr, 0)
     elapsed = max_over_ranks(elapsed, dist, device)
@@ -197,14 +197,14 @@ def main():
     t_one = timed(lambda: (nice.encode_batch(one_px, W, H, 4, one_s, one_l),
                            nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st)), reps=2)
 
-    names = [L.nice_phase_name(i).decode() for i in range(12)]
+    names = [L.nice_phase_name(i).decode() for i in range(32)]
     phase = {names[i]: {"ms_total": round(ms[i], 3), "launches": int(cnt[i])}
-             for i in range(12) if cnt[i]}
+             for i in range(32) if cnt[i] and names[i]}
     # dominant kernel and its algorithmic bytes per launch
     in_bytes = F * N * 4
     out_px_bytes = F * N * 4
     algo = {
-        "enc_classify": in_bytes, "enc_pack": in_bytes + stream_bytes,
+        "enc_classify": in_bytes, "enc_pack": stream_bytes,
         "dec_sync": stream_bytes, "dec_emit": stream_bytes,
         "dec_reconstruct": out_px_bytes,
     }

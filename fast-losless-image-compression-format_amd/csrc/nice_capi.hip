@@ -48,19 +48,17 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Encoder scratch layout. The zero-per-launch block comes first (memset once).
 struct EncLayout {
   size_t zero_bytes, total;
-  size_t o_hist, o_flags, o_ticket, o_desc;
+  size_t o_hist, o_flags;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend;
 };
 
-EncLayout enc_layout(uint32_t n_frames, uint32_t T) {
+EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   EncLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
   L.o_hist = take((size_t)n_frames * N_BINS * 4);
   L.o_flags = take((size_t)n_frames * 4);
-  L.o_ticket = take(16);
-  L.o_desc = take((size_t)n_frames * T * 16);
   L.zero_bytes = align_up(o, 16);
   L.o_first = take((size_t)n_frames * T * 4);
   L.o_last = take((size_t)n_frames * T * 4);
@@ -74,6 +72,10 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T) {
   L.o_hdrbytes = take((size_t)n_frames * 8);
   L.o_hdrcache = take((size_t)n_frames * 4);
   L.o_hdrbitoff = take((size_t)n_frames);
+  L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
+  L.o_tbits = take((size_t)n_frames * T * 4);
+  L.o_toff = take((size_t)n_frames * T * 8);
+  L.o_dend = take((size_t)n_frames * 8);
   L.total = o;
   return L;
 }
@@ -90,8 +92,9 @@ int check_device(int device) {
 }  // namespace
 
 static const char* kPhaseNames[NICE_PHASES] = {
-    "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_pack", "enc_serial",
-    "dec_tables", "dec_sync", "dec_count", "dec_scan", "dec_emit", "dec_reconstruct"};
+    "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_tilebits", "enc_tilescan",
+    "enc_pack", "enc_tail", "enc_serial", "dec_tables", "dec_sync", "dec_scan", "dec_emit",
+    "dec_reconstruct"};
 
 // Optional per-phase HIP-event timing (bench / profiling).
 struct PhaseTimer {
@@ -192,7 +195,7 @@ static uint32_t tiles_for(uint32_t w, uint32_t h) {
 int nice_ctx_reserve(nice_ctx* ctx, uint32_t n_frames, uint32_t w, uint32_t h) {
   if (!ctx) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
-  EncLayout L = enc_layout(n_frames, tiles_for(w, h));
+  EncLayout L = enc_layout(n_frames, tiles_for(w, h), (uint64_t)w * h);
   return ctx->enc.grow(L.total);
 }
 
@@ -213,7 +216,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   const uint32_t T = tiles_for(w, h);
-  EncLayout L = enc_layout(n_frames, T);
+  EncLayout L = enc_layout(n_frames, T, N);
   int rc = ctx->enc.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->enc.ptr;
@@ -231,8 +234,6 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   a.out_len = (unsigned long long*)d_out_len;
   a.hist = (uint32_t*)(base + L.o_hist);
   a.frame_flags = (uint32_t*)(base + L.o_flags);
-  a.ticket = (uint32_t*)(base + L.o_ticket);
-  a.tiles_desc = base + L.o_desc;
   a.tile_first = (uint32_t*)(base + L.o_first);
   a.tile_last = (uint32_t*)(base + L.o_last);
   a.tile_next = (uint32_t*)(base + L.o_next);
@@ -245,6 +246,11 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   a.hdr_bytes = (unsigned long long*)(base + L.o_hdrbytes);
   a.hdr_cache = (uint32_t*)(base + L.o_hdrcache);
   a.hdr_bitoff = base + L.o_hdrbitoff;
+  a.recs = (uint32_t*)(base + L.o_recs);
+  a.rec_stride = (N + 3) & ~3ull;
+  a.tile_bits = (uint32_t*)(base + L.o_tbits);
+  a.tile_off = (unsigned long long*)(base + L.o_toff);
+  a.data_end = (unsigned long long*)(base + L.o_dend);
 
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
   const uint64_t total_tiles = (uint64_t)n_frames * T;
@@ -271,10 +277,19 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   hipLaunchKernelGGL(enc_header, dim3(n_frames), dim3(64), 0, st, a);
   ctx->timer.end(st);
   if (T > 0) {
+    // grid-stride over tiles: 8 blocks of 256 threads per CU (LDS ~21 KB each)
+    const uint32_t tblocks = (uint32_t)(total_tiles < 2048 ? total_tiles : 2048);
+    ctx->timer.begin(NICE_PH_ENC_TILEBITS, st);
+    hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
+    ctx->timer.end(st);
+    ctx->timer.begin(NICE_PH_ENC_TILESCAN, st);
+    hipLaunchKernelGGL(enc_tilescan, dim3(n_frames), dim3(1024), 0, st, a);
+    ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_PACK, st);
-    // persistent blocks in ticket order; <= 4 resident per CU (LDS ~37 KB each)
-    const uint64_t pblocks = total_tiles < 1024 ? total_tiles : 1024;
-    hipLaunchKernelGGL(enc_pack, dim3((uint32_t)pblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
+    ctx->timer.end(st);
+    ctx->timer.begin(NICE_PH_ENC_TAIL, st);
+    hipLaunchKernelGGL(enc_tail, dim3((n_frames + 63) / 64), dim3(64), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_SERIAL, st);
     hipLaunchKernelGGL(enc_serial, dim3(n_frames), dim3(64), 0, st, a);
@@ -475,7 +490,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
-  tm.begin(NICE_PH_DEC_BOUNDS, st);
+  tm.begin(NICE_PH_DEC_EMIT, st);
   NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
   hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a);
   tm.end(st);

@@ -85,8 +85,92 @@ __device__ __forceinline__ int next_coded_local(const uint32_t* mask, int p) {
 }
 
 // ---------------------------------------------------------------------------
-// K1: classify + histogram.
+// K1: classify + histogram + per-pixel symbol records.
+//
+// Record (one u32 per pixel, raster order): bits 0..2 the mode prefix
+// (P_BACK_REF .. P_LUMA2) or REC_UNCODED for a run member; bits 3.. the payload:
+//   BACK_REF  k (3)                 SMALL_DIFF  index 0..342 (9)
+//   LUMA2     g+32 (6), r+16 (5), b+16 (5)
+//   LUMA      k (4), g+32 (6), r+16 (5), b+16 (5)
+//   RGB       r, g, b residuals (8 each)
 // ---------------------------------------------------------------------------
+constexpr uint32_t REC_UNCODED = 7u;
+
+__device__ __forceinline__ uint32_t rec_from_syms(const PixSyms& s) {
+  switch (s.mode) {
+    case P_BACK_REF: return P_BACK_REF | ((s.b[0] - BIN_BACK_REF) << 3);
+    case P_SMALL_DIFF: return P_SMALL_DIFF | ((s.b[0] - BIN_SMALL_DIFF) << 3);
+    case P_LUMA2:
+      return P_LUMA2 | ((s.b[0] - BIN_LUMA2_BASE) << 3) | ((s.b[1] - BIN_LUMA2_R) << 9) |
+             ((s.b[2] - BIN_LUMA2_B) << 14);
+    case P_LUMA:
+      return P_LUMA | ((s.b[0] - BIN_LUMA_REF) << 3) | ((s.b[1] - BIN_LUMA_BASE) << 7) |
+             ((s.b[2] - BIN_LUMA_OTHER) << 13) | ((s.b[3] - BIN_LUMA_OTHER) << 18);
+    default: return P_RGB | (s.b[0] << 3) | (s.b[1] << 11) | (s.b[2] << 19);
+  }
+}
+
+// Payload bins of a coded record (n = 1, 3 or 4), branch-free.
+__device__ __forceinline__ uint32_t rec_bins(uint32_t rec, uint32_t& b0, uint32_t& b1, uint32_t& b2,
+                                             uint32_t& b3) {
+  const uint32_t m = rec & 7u;
+  const uint32_t x = rec >> 3;
+  const bool br = m == P_BACK_REF, sd = m == P_SMALL_DIFF, l2 = m == P_LUMA2, lu = m == P_LUMA;
+  b0 = br ? BIN_BACK_REF + (x & 7u)
+     : sd ? BIN_SMALL_DIFF + (x & 511u)
+     : l2 ? BIN_LUMA2_BASE + (x & 63u)
+     : lu ? BIN_LUMA_REF + (x & 15u) : (x & 255u);
+  b1 = l2 ? BIN_LUMA2_R + ((x >> 6) & 31u) : lu ? BIN_LUMA_BASE + ((x >> 4) & 63u) : ((x >> 8) & 255u);
+  b2 = l2 ? BIN_LUMA2_B + ((x >> 11) & 31u) : lu ? BIN_LUMA_OTHER + ((x >> 10) & 31u) : ((x >> 16) & 255u);
+  b3 = BIN_LUMA_OTHER + ((x >> 15) & 31u);
+  return (br || sd) ? 1u : lu ? 4u : 3u;
+}
+
+// Branch-free mode decision for a pixel whose every reference exists
+// (i >= 3W+3, W >= 3): all tests are evaluated and the first hit in the
+// reference order wins (code.rs:191-366).  Neighbours come from the LDS windows
+// (column col = p + 3 of window `rows`, pixel i - (rows*W + px) at col - px).
+__device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col) {
+  const uint32_t X = tw.w[0][col], L = tw.w[0][col - 1], L2 = tw.w[0][col - 2], L3 = tw.w[0][col - 3];
+  const uint32_t U = tw.w[1][col], UR1 = tw.w[1][col + 1], UR3 = tw.w[1][col + 3], UL3 = tw.w[1][col - 3];
+  const uint32_t U2 = tw.w[2][col];
+  const uint32_t V = tw.w[3][col], VR1 = tw.w[3][col + 1], VL1 = tw.w[3][col - 1];
+  const uint32_t VL3 = tw.w[3][col - 3], VR3 = tw.w[3][col + 3];
+  // back references k = 1..4 (k = 0, the pixel before, never equals a coded pixel)
+  const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  const bool br = e1 | e2 | e3 | e4;
+  const uint32_t bk = e1 ? 1u : e2 ? 2u : e3 ? 3u : 4u;
+  const uint32_t pred = avg3(U, L);
+  // small diff
+  const uint32_t d = X + K3(259u) - pred;
+  const bool sd = ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
+  const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
+  // luma2 against the average
+  const uint32_t xk = X + LUMA_K;
+  const uint32_t t2 = luma_t(xk, pred);
+  const bool l2 = (t2 & LUMA_MASK) == 0;
+  // luma against 11 references, first hit wins; skipped when no lane needs it
+  uint32_t lk = 11u, lt = 0u;
+  if (__any(!br && !sd && !l2)) {
+    const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
+#pragma unroll
+    for (int k = 10; k >= 0; --k) {
+      const uint32_t t = luma_t(xk, refs[k]);
+      const bool ok = (t & LUMA_MASK) == 0;
+      lk = ok ? (uint32_t)k : lk;
+      lt = ok ? t : lt;
+    }
+  }
+  const uint32_t r = X + K3(256u) - pred;
+  const uint32_t rec_br = P_BACK_REF | (bk << 3);
+  const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
+  const uint32_t rec_l2 = P_LUMA2 | (((t2 >> 10) & 63u) << 3) | ((t2 & 31u) << 9) | (((t2 >> 20) & 31u) << 14);
+  const uint32_t rec_lu = P_LUMA | (lk << 3) | (((lt >> 10) & 63u) << 7) | ((lt & 31u) << 13) |
+                          (((lt >> 20) & 31u) << 18);
+  const uint32_t rec_rgb = P_RGB | ((r & 255u) << 3) | (((r >> 10) & 255u) << 11) | (((r >> 20) & 255u) << 19);
+  return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
+}
+
 __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
   __shared__ TileWin tw;
   __shared__ uint32_t hist[N_BINS];
@@ -148,19 +232,28 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
       a.tile_last[t] = last < 0 ? NONE : (uint32_t)(start + last);
     }
     const bool fast = (a.W >= 3) && (start >= 3 * (int64_t)a.W + 3);
+    uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
 #pragma unroll
     for (int r = 0; r < PX_PER_THREAD; ++r) {
       const int p = r * ENC_THREADS + threadIdx.x;
       const bool coded = (coded_bits >> r) & 1u;
-      PixSyms s;
-      s.mode = 0xFF;
-      if (coded) {
+      uint32_t rec = REC_UNCODED;
+      if (fast) {
+        const uint32_t rf = classify_fast(tw, p + 3);
+        rec = coded ? rf : REC_UNCODED;
+      } else if (coded) {
+        PixSyms s;
         WinAcc acc{&tw, p + 3};
-        if (fast) classify<true>((uint32_t)(start + p), a.W, acc, s);
-        else classify<false>((uint32_t)(start + p), a.W, acc, s);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if ((uint32_t)k < s.n) atomicAdd(&hist[s.b[k]], 1u);
+        classify<false>((uint32_t)(start + p), a.W, acc, s);
+        rec = rec_from_syms(s);
+      }
+      if (p < count) recs[p] = rec;
+      if (coded) {
+        uint32_t b0, b1, b2, b3;
+        const uint32_t n = rec_bins(rec, b0, b1, b2, b3);
+        atomicAdd(&hist[b0], 1u);
+        if (n > 1) { atomicAdd(&hist[b1], 1u); atomicAdd(&hist[b2], 1u); }
+        if (n > 3) atomicAdd(&hist[b3], 1u);
         const int nx = next_coded_local(mask, p);
         if (nx < count) {
           const uint64_t run = (uint64_t)(nx - p - 1);
@@ -177,7 +270,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
       // mode prefix: aggregate per wave (5 values, heavy contention otherwise)
 #pragma unroll
       for (int v = 0; v < 5; ++v) {
-        const unsigned long long bal = __ballot(s.mode == (uint32_t)v);
+        const unsigned long long bal = __ballot(coded && (rec & 7u) == (uint32_t)v);
         if (lane == v && bal) atomicAdd(&hist[BIN_PREFIX + v], (uint32_t)__popcll(bal));
       }
     }
@@ -384,9 +477,10 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
       pos += 7u * n;
     }
     __syncthreads();
-    // pos == 104 + 6056 = 6160; write words [0, 192) (bytes 0..767)
-    const uint32_t full = pos >> 5;
-    for (int w = lane; w < (int)full; w += 64)
+    // pos == 104 + 6056 = 6160; write words [0, 193): the last one partial,
+    // zero past the header (the first data tile ORs into it)
+    const uint32_t nwords = (pos + 31) >> 5;
+    for (int w = lane; w < (int)nwords; w += 64)
       reinterpret_cast<uint32_t*>(out)[w] = __builtin_bswap32(words[w]);
     if (lane == 0) {
       a.seed_bit[f] = pos;
@@ -422,6 +516,13 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
   uint32_t suf = (uint32_t)acc;
   if (bw.bit_offset) suf = (suf << bw.bit_offset) | (bw.cache >> (32 - bw.bit_offset));
   a.seed_suf[f] = suf;
+  if (!serial_frame && N > 0) {
+    // pending bits (top bit_offset bits of the cache), then zeros to the end of
+    // the word holding the data start: the first data tile ORs into it
+    const uint64_t wend = ((pos >> 5) + 1) * 4;
+    out[bw.pos] = bw.bit_offset ? (uint8_t)((bw.cache >> 24) & (0xFFu << (8 - bw.bit_offset))) : 0u;
+    for (uint64_t q = bw.pos + 1; q < wend; ++q) out[q] = 0;
+  }
   if (N == 0 && !serial_frame) {
     // no data symbols: tail only (hfe.rs:115, code.rs:421-422)
     const uint8_t P = (uint8_t)(bw.cache >> 24);
@@ -436,316 +537,257 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K5: pack with decoupled look-back.
+// K5-K7: bit placement without a serial dependency.
+//   enc_tilebits  per tile: bits of its pixels (prefix, payload, run digits)
+//   enc_tilescan  per frame: exclusive scan of tile bits from the data start;
+//                 zeroes every output word two tiles (or a tile and the tail)
+//                 share, so enc_pack can OR those and store the rest
+//   enc_pack      per tile: codes MSB-first into an LDS bit buffer, then
+//                 shifted to the tile's offset: interior words stored, the
+//                 first/last partial words OR-ed (bitwriter.rs:55-73)
+//   enc_tail      per frame: [P, P, 0, 0, 0] after the data (hfe.rs:115,
+//                 code.rs:421-422) and the stream length
+// A thread owns 4 consecutive pixels and reads their records with one 16-byte
+// load.
 // ---------------------------------------------------------------------------
-constexpr uint64_t ST_AGG = 1ull << 62;
-constexpr uint64_t ST_INC = 2ull << 62;
-constexpr uint64_t LEN_MASK = (1ull << 62) - 1;
-// per tile: {u64 flag, u32 suffix_agg, u32 suffix_inc}
-struct TileDesc {
-  unsigned long long flag;
-  uint32_t suf_agg;
-  uint32_t suf_inc;
-};
-
-__device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx64(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_rlx64(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// (len, last-32-bits) monoid
-__device__ __forceinline__ void suf_combine(uint64_t& len, uint32_t& suf, uint64_t len2, uint32_t suf2) {
-  if (len2 >= 32) suf = suf2;
-  else if (len2 > 0) suf = (suf << len2) | suf2;
-  len += len2;
-}
-
 constexpr int PACK_MAX_WORDS = ENC_TILE * 128 / 32 + 2;   // <= 125 bits/px with 25-bit codes
 
-__device__ __forceinline__ void or_bits(uint32_t* buf, uint64_t pos, uint32_t v, uint32_t n) {
-  // place the low n (1..32) bits of v at local bit position pos (MSB-first)
-  const uint32_t w = (uint32_t)(pos >> 5), o = (uint32_t)(pos & 31);
-  if (o + n <= 32) {
-    atomicOr(&buf[w], v << (32 - o - n));
+struct TileQuad {
+  uint32_t rc[4];
+  uint32_t nib;        // coded flags of the 4 pixels
+  uint64_t run[4];     // run after each coded pixel
+  uint32_t nb;         // bits of the 4 pixels
+};
+
+// Loads the thread's 4 records, builds the tile's coded mask (LDS, needs a
+// barrier before use) -- phase 1.
+__device__ __forceinline__ void quad_load(const EncArgs& a, uint32_t f, int64_t start, int count, int p0,
+                                          int lane, int wid, uint32_t* mask, TileQuad& Q) {
+  const uint32_t* rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
+  if (p0 + 3 < count) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rp);
+    Q.rc[0] = v.x; Q.rc[1] = v.y; Q.rc[2] = v.z; Q.rc[3] = v.w;
   } else {
-    atomicOr(&buf[w], v >> (o + n - 32));
-    atomicOr(&buf[w + 1], v << (64 - o - n));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Q.rc[q] = (p0 + q < count) ? rp[q] : REC_UNCODED;
+  }
+  Q.nib = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Q.nib |= ((Q.rc[q] & 7u) != REC_UNCODED ? 1u : 0u) << q;
+  uint32_t mw = Q.nib << (4 * (lane & 7));
+  mw |= __shfl_xor(mw, 1);
+  mw |= __shfl_xor(mw, 2);
+  mw |= __shfl_xor(mw, 4);
+  if ((lane & 7) == 0) mask[wid * 8 + (lane >> 3)] = mw;
+}
+
+// Runs and bit counts -- phase 2 (after the mask barrier).
+__device__ __forceinline__ void quad_bits(const uint32_t* tbl, const uint32_t* mask, int64_t start, int count,
+                                          int p0, uint32_t next_tile_px, TileQuad& Q) {
+  const int nx_local = next_coded_local(mask, p0 + 3);
+  const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)next_tile_px;
+  Q.nb = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    Q.run[q] = 0;
+    if ((Q.nib >> q) & 1u) {
+      const uint32_t later = Q.nib >> (q + 1);
+      const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
+      Q.run[q] = nxt - (uint64_t)(start + p0 + q) - 1;
+      uint32_t b0, b1, b2, b3;
+      const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
+      Q.nb += (tbl[BIN_PREFIX + (Q.rc[q] & 7u)] & 31u) + (tbl[b0] & 31u);
+      if (n > 1) Q.nb += (tbl[b1] & 31u) + (tbl[b2] & 31u);
+      if (n > 3) Q.nb += tbl[b3] & 31u;
+      if (Q.run[q] > 0) {
+        uint64_t m = Q.run[q] - 1;
+        while (true) {
+          Q.nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
+          if (m < 8) break;
+          m >>= 3;
+        }
+      }
+    }
   }
 }
 
-// Wave-parallel decoupled look-back for tile t (wave 0 only): lane i inspects
-// predecessor t-1-i; a window without an inclusive prefix folds 64 aggregates
-// and moves back 64 tiles.  Returns the exclusive (bit length, last 32 bits).
-__device__ inline void look_back(const EncArgs& a, uint64_t t, uint32_t tt, uint32_t f, int lane,
-                                 uint64_t* wlen, uint32_t* wsuf, uint64_t* out_len, uint32_t* out_suf) {
-  TileDesc* desc = reinterpret_cast<TileDesc*>(a.tiles_desc);
-  const int64_t fs = (int64_t)t - tt;           // first tile of this frame
-  uint64_t acc_len = 0;                         // tiles (base+1 .. t-1), concatenated
-  uint32_t acc_suf = 0;
-  int64_t base = (int64_t)t - 1;
-  uint32_t spins = 0;
-  while (true) {
-    const int64_t j = base - lane;
-    uint64_t st, len;
-    uint32_t suf = 0;
-    if (j < fs) {                               // before the frame: the header seed
-      st = ST_INC;
-      len = a.seed_bit[f];
-    } else {
-      const unsigned long long fl = ld_rlx64(&desc[j].flag);
-      st = fl & ~LEN_MASK;
-      len = fl & LEN_MASK;
-    }
-    const unsigned long long inc = __ballot(st == ST_INC);
-    const int first_inc = inc ? __builtin_ctzll(inc) : 64;
-    const unsigned long long need = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1ull);
-    if (__ballot(st == 0) & need) {
-      if (++spins > 16) __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    if (lane <= first_inc) {
-      if (j < fs) suf = a.seed_suf[f];
-      else suf = st == ST_INC ? ld_rlx(&desc[j].suf_inc) : ld_rlx(&desc[j].suf_agg);
-      wlen[lane] = len;
-      wsuf[lane] = suf;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (lane == 0) {
-      const int last = first_inc < 64 ? first_inc : 63;
-      uint64_t l = 0;
-      uint32_t sx = 0;
-      for (int i = last; i >= 0; --i) suf_combine(l, sx, wlen[i], wsuf[i]);   // oldest first
-      suf_combine(l, sx, acc_len, acc_suf);
-      acc_len = l;
-      acc_suf = sx;
-    }
-    acc_len = __shfl(acc_len, 0);
-    acc_suf = __shfl(acc_suf, 0);
-    if (first_inc < 64) break;
-    base -= 64;
-  }
-  *out_len = acc_len;
-  *out_suf = acc_suf;
+__device__ __forceinline__ void load_tbl(uint32_t* tbl, const EncArgs& a, uint32_t f) {
+  for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
 }
 
-// Persistent: each block takes tiles in ticket order (forward progress for the
-// look-back), reloading the code table only when the frame changes.
+__global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
+  __shared__ uint32_t tbl[N_BINS];
+  __shared__ uint32_t mask[ENC_TILE / 32];
+  __shared__ uint32_t wsum[ENC_THREADS / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t T = a.tiles_per_frame;
+  const uint64_t total = (uint64_t)a.n_frames * T;
+  const int64_t N = (int64_t)a.W * a.H;
+  const int p0 = 4 * threadIdx.x;
+  uint32_t cur_f = 0xFFFFFFFFu;
+  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+    const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
+    const int64_t start = (int64_t)tt * ENC_TILE;
+    const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+    __syncthreads();
+    if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
+    TileQuad Q;
+    quad_load(a, f, start, count, p0, lane, wid, mask, Q);
+    __syncthreads();
+    quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
+    uint32_t x = Q.nb;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) wsum[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) a.tile_bits[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  }
+}
+
+// One 1024-thread block per frame.
+__global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
+  __shared__ unsigned long long part[1024];
+  const uint32_t f = blockIdx.x;
+  if (a.frame_flags[f] & FLAG_SERIAL) return;
+  const uint32_t T = a.tiles_per_frame;
+  const uint64_t base = (uint64_t)f * T;
+  const uint32_t per = (T + 1023) / 1024;
+  const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, T);
+  unsigned long long sum = 0;
+  for (uint32_t t = c0; t < c1; ++t) sum += a.tile_bits[base + t];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const unsigned long long v = (int)threadIdx.x >= d ? part[threadIdx.x - d] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint64_t seed = a.seed_bit[f];
+  const uint64_t seed_word = seed >> 5;
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
+  unsigned long long run = seed + (threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+  for (uint32_t t = c0; t < c1; ++t) {
+    a.tile_off[base + t] = run;
+    // a word shared with the previous tile (or the header: pre-padded with zeros)
+    if ((run & 31) && (run >> 5) > seed_word) out32[run >> 5] = 0u;
+    run += a.tile_bits[base + t];
+  }
+  if (threadIdx.x == 1023) {
+    const uint64_t end = seed + part[1023];
+    a.data_end[f] = end;
+    if ((end & 31) && (end >> 5) > seed_word) out32[end >> 5] = 0u;
+  }
+}
+
 __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
-  __shared__ TileWin tw;
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
-  __shared__ uint64_t wlen[64];
-  __shared__ uint32_t wsuf[64];
-  __shared__ uint32_t s_tile;
-  __shared__ uint64_t s_excl_len;
-  __shared__ uint32_t s_excl_suf;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total = (uint64_t)a.n_frames * T;
   const int64_t N = (int64_t)a.W * a.H;
+  const int p0 = 4 * threadIdx.x;
   uint32_t cur_f = 0xFFFFFFFFu;
-  uint32_t used_words = PACK_MAX_WORDS;        // bits[] words to clear before the next tile
-  TileDesc* descs = reinterpret_cast<TileDesc*>(a.tiles_desc);
-
-  while (true) {
-    __syncthreads();
-    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
-    for (uint32_t w = threadIdx.x; w < used_words; w += ENC_THREADS) bits[w] = 0;
-    __syncthreads();
-    const uint64_t t = s_tile;
-    if (t >= total) break;
-    const uint32_t f = (uint32_t)(t / T);
-    const uint32_t tt = (uint32_t)(t % T);
-    if (a.frame_flags[f] & FLAG_SERIAL) { used_words = 0; continue; }   // enc_serial's frame
-    const uint8_t* frame = a.px + (uint64_t)f * a.frame_stride;
+  uint32_t used_words = PACK_MAX_WORDS;
+  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+    const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // enc_serial's frame
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
-    if (f != cur_f) {
-      for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
-      cur_f = f;
-    }
-    stage_tile(tw, frame, start, N, a.W, a.C);
     __syncthreads();
-
-    uint32_t coded_bits = 0;
-#pragma unroll
-    for (int r = 0; r < PX_PER_THREAD; ++r) {
-      const int p = r * ENC_THREADS + threadIdx.x;
-      const int64_t i = start + p;
-      bool coded = false;
-      if (p < count) coded = (i == 0) || (tw.w[0][p + 3] != tw.w[0][p + 2]);
-      const unsigned long long bal = __ballot(coded);
-      if (lane == 0) {
-        const int wbase = (r * ENC_THREADS + (threadIdx.x & ~63)) >> 5;
-        mask[wbase] = (uint32_t)bal;
-        mask[wbase + 1] = (uint32_t)(bal >> 32);
-      }
-      coded_bits |= (coded ? 1u : 0u) << r;
-    }
+    for (uint32_t w = threadIdx.x; w < used_words; w += ENC_THREADS) bits[w] = 0;
+    if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
+    TileQuad Q;
+    quad_load(a, f, start, count, p0, lane, wid, mask, Q);
     __syncthreads();
-
-    const bool fast = (a.W >= 3) && (start >= 3 * (int64_t)a.W + 3);
-    const uint32_t next_tile_px = a.tile_next[t];
-    uint32_t round_base = 0;
+    quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
+    uint32_t x = Q.nb;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y2 = __shfl_up(x, o);
+      if (lane >= o) x += y2;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tile_bits = 0;
 #pragma unroll
-    for (int r = 0; r < PX_PER_THREAD; ++r) {
-      const int p = r * ENC_THREADS + threadIdx.x;
-      PixSyms sy;
-      sy.n = 0;
-      sy.mode = 0;
-      uint64_t run = 0;
-      uint32_t nb = 0;
-      if ((coded_bits >> r) & 1u) {
-        WinAcc acc{&tw, p + 3};
-        if (fast) classify<true>((uint32_t)(start + p), a.W, acc, sy);
-        else classify<false>((uint32_t)(start + p), a.W, acc, sy);
-        nb = tbl[BIN_PREFIX + sy.mode] & 31u;
+    for (int w = 0; w < ENC_THREADS / 64; ++w) {
+      const uint32_t ws = wsum[w];
+      wbase += (w < wid) ? ws : 0u;
+      tile_bits += ws;
+    }
+    if (Q.nb) {
+      const uint32_t pos = wbase + x - Q.nb;
+      uint64_t acc = 0;
+      uint32_t nacc = pos & 31u, wi = pos >> 5;
+      auto put = [&](uint32_t e) {
+        const uint32_t n = e & 31u;
+        acc |= (uint64_t)(e >> 5) << (64u - nacc - n);
+        nacc += n;
+        if (nacc >= 32u) {
+          atomicOr(&bits[wi], (uint32_t)(acc >> 32));
+          acc <<= 32;
+          nacc -= 32u;
+          ++wi;
+        }
+      };
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if ((uint32_t)k < sy.n) nb += tbl[sy.b[k]] & 31u;
-        const int nx = next_coded_local(mask, p);
-        const uint64_t nxt = (nx < count) ? (uint64_t)(start + nx) : (uint64_t)next_tile_px;
-        run = nxt - (uint64_t)(start + p) - 1;
-        if (run > 0) {
-          uint64_t m = run - 1;
-          while (true) {
-            nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
-            if (m < 8) break;
-            m >>= 3;
+      for (int q = 0; q < 4; ++q) {
+        if ((Q.nib >> q) & 1u) {
+          uint32_t b0, b1, b2, b3;
+          const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
+          put(tbl[BIN_PREFIX + (Q.rc[q] & 7u)]);
+          put(tbl[b0]);
+          if (n > 1) { put(tbl[b1]); put(tbl[b2]); }
+          if (n > 3) put(tbl[b3]);
+          if (Q.run[q] > 0) {
+            uint64_t m = Q.run[q] - 1;
+            while (true) {
+              put(tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)]);
+              if (m < 8) break;
+              m >>= 3;
+            }
           }
         }
       }
-      // block-wide exclusive scan of this round's pixel bit lengths
-      uint32_t x = nb;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y2 = __shfl_up(x, o);
-        if (lane >= o) x += y2;
-      }
-      if (lane == 63) wsum[wid] = x;
-      __syncthreads();
-      uint32_t wbase = 0, rtotal = 0;
-#pragma unroll
-      for (int w = 0; w < ENC_THREADS / 64; ++w) {
-        const uint32_t ws = wsum[w];
-        wbase += (w < wid) ? ws : 0u;
-        rtotal += ws;
-      }
-      const uint32_t excl = round_base + wbase + x - nb;
-      round_base += rtotal;
-      __syncthreads();
-      // assemble this pixel's bits (MSB-first) into the tile buffer
-      if (nb) {
-        uint64_t pos = excl;
-        uint32_t e = tbl[BIN_PREFIX + sy.mode];
-        or_bits(bits, pos, e >> 5, e & 31u);
-        pos += e & 31u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if ((uint32_t)k < sy.n) {
-            e = tbl[sy.b[k]];
-            or_bits(bits, pos, e >> 5, e & 31u);
-            pos += e & 31u;
-          }
-        }
-        if (run > 0) {
-          uint64_t m = run - 1;
-          while (true) {
-            e = tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
-            or_bits(bits, pos, e >> 5, e & 31u);
-            pos += e & 31u;
-            if (m < 8) break;
-            m >>= 3;
-          }
-        }
-      }
-    }
-    const uint32_t tile_bits = round_base;
-    __syncthreads();
-
-    if (wid == 0) {
-      // local last 32 bits
-      uint32_t suf = 0;
-      if (tile_bits > 0) {
-        const uint32_t endw = (tile_bits - 1) >> 5;
-        const uint32_t o = tile_bits & 31;
-        if (o == 0) suf = bits[endw];
-        else suf = ((endw ? bits[endw - 1] : 0u) << o) | (bits[endw] >> (32 - o));
-        if (tile_bits < 32) suf &= (1u << tile_bits) - 1u;
-      }
-      TileDesc* desc = descs + t;
-      uint64_t excl_len;
-      uint32_t excl_suf;
-      if (tt == 0) {
-        excl_len = a.seed_bit[f];
-        excl_suf = a.seed_suf[f];
-      } else {
-        if (lane == 0) {
-          st_rlx(&desc->suf_agg, suf);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          st_rlx64(&desc->flag, ST_AGG | tile_bits);
-        }
-        look_back(a, t, tt, f, lane, wlen, wsuf, &excl_len, &excl_suf);
-      }
-      if (lane == 0) {
-        uint64_t inc_len = excl_len;
-        uint32_t inc_suf = excl_suf;
-        suf_combine(inc_len, inc_suf, tile_bits, suf);
-        st_rlx(&desc->suf_inc, inc_suf);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_rlx64(&desc->flag, ST_INC | inc_len);
-        s_excl_len = excl_len;
-        s_excl_suf = excl_suf;
-      }
+      if (nacc) atomicOr(&bits[wi], (uint32_t)(acc >> 32));
     }
     __syncthreads();
-    const uint64_t s0 = s_excl_len;
-    const uint32_t suf0 = s_excl_suf;
-    const uint64_t e0 = s0 + tile_bits;
-    const uint64_t w0 = s0 >> 5, w1 = e0 >> 5;
+    // place the tile's bits at its stream offset
+    const uint64_t s0 = a.tile_off[t], e0 = s0 + tile_bits;
     const uint32_t sh = (uint32_t)(s0 & 31);
-    uint8_t* out = a.out + (uint64_t)f * a.out_stride;
-    uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
-    // word w0+m = (prev : bits[m]) >> sh, prev = bits[m-1] or the exclusive suffix
-    for (uint64_t m = threadIdx.x; m < w1 - w0; m += ENC_THREADS) {
-      const uint32_t hi = m ? bits[m - 1] : suf0;
-      const uint32_t lo = bits[m];
+    const uint64_t w0 = s0 >> 5;
+    const uint32_t nw = tile_bits ? (uint32_t)(((e0 + 31) >> 5) - w0) : 0u;
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
+    for (uint32_t m = threadIdx.x; m < nw; m += ENC_THREADS) {
+      const uint32_t hi = m ? bits[m - 1] : 0u;
+      const uint32_t lo = bits[m];   // zero past the tile's bits
       const uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
-      out32[w0 + m] = __builtin_bswap32(v);
+      const bool shared = (m == 0 && sh) || (m == nw - 1 && (e0 & 31));
+      if (shared) atomicOr(&out32[w0 + m], __builtin_bswap32(v));
+      else out32[w0 + m] = __builtin_bswap32(v);
     }
-    if (tt == T - 1 && threadIdx.x == 0) {
-      // tail: partial word w1, then [P, P, 0, 0, 0] (hfe.rs:115, code.rs:421-422)
-      const uint64_t m = w1 - w0;
-      const uint32_t hi = m ? bits[m - 1] : suf0;
-      const uint32_t lo = bits[m];
-      uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
-      const uint32_t q = (uint32_t)(e0 & 31);
-      v = q ? (v & (0xFFFFFFFFu << (32 - q))) : 0u;
-      const uint64_t B = e0 >> 3;              // index of the partial/cache byte
-      uint64_t pp = w1 * 4;
-      for (; pp < B; ++pp) out[pp] = (uint8_t)(v >> (24 - 8 * (pp - w1 * 4)));
-      const uint8_t P = (e0 & 7) ? (uint8_t)(v >> (24 - 8 * (B - w1 * 4))) : 0u;
-      out[B] = P;
-      out[B + 1] = P;
-      out[B + 2] = 0;
-      out[B + 3] = 0;
-      out[B + 4] = 0;
-      a.out_len[f] = B + 5;
-    }
-    used_words = (uint32_t)(w1 - w0 + 2);
+    used_words = nw + 1;
   }
+}
+
+__global__ __launch_bounds__(64) void enc_tail(EncArgs a) {
+  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+  if (f >= a.n_frames) return;
+  if ((a.frame_flags[f] & FLAG_SERIAL) || (uint64_t)a.W * a.H == 0) return;
+  uint8_t* out = a.out + (uint64_t)f * a.out_stride;
+  const uint64_t e0 = a.data_end[f];
+  const uint64_t B = e0 >> 3;            // the partial byte (the reference's cache >> 24)
+  const uint8_t P = (e0 & 7) ? out[B] : 0u;
+  out[B] = P;
+  out[B + 1] = P;
+  out[B + 2] = 0;
+  out[B + 3] = 0;
+  out[B + 4] = 0;
+  a.out_len[f] = B + 5;
 }
 
 // ---------------------------------------------------------------------------

@@ -35,15 +35,21 @@ struct EncArgs {
   unsigned long long* hdr_bytes;  // n_frames (serial header path)
   uint32_t* hdr_cache;       // n_frames
   uint8_t* hdr_bitoff;       // n_frames
-  void* tiles_desc;          // n_frames * T * 16 bytes, zeroed per launch
-  uint32_t* ticket;          // zeroed per launch
+  uint32_t* recs;            // n_frames * rec_stride per-pixel symbol records
+  uint64_t rec_stride;       // W*H rounded up to 4
+  uint32_t* tile_bits;       // n_frames * T: data bits per tile
+  unsigned long long* tile_off;   // n_frames * T: absolute bit offset of each tile
+  unsigned long long* data_end;   // n_frames: bit position after the last data bit
 };
 
 __global__ void enc_classify(EncArgs a);
 __global__ void enc_tailruns(EncArgs a);
 __global__ void enc_tables(EncArgs a);
 __global__ void enc_header(EncArgs a);
+__global__ void enc_tilebits(EncArgs a);
+__global__ void enc_tilescan(EncArgs a);
 __global__ void enc_pack(EncArgs a);
+__global__ void enc_tail(EncArgs a);
 __global__ void enc_serial(EncArgs a);
 
 }  // namespace nice
