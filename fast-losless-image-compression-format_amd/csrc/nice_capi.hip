@@ -490,6 +490,12 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
+  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
+  unsigned long long* dstats = nullptr;
+  if (want_stats && hipMalloc(&dstats, 256) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 256, st);
+    a.stats = dstats;
+  }
   tm.begin(NICE_PH_DEC_EMIT, st);
   NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
   hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a);
@@ -497,12 +503,6 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
-  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
-  unsigned long long* dstats = nullptr;
-  if (want_stats && hipMalloc(&dstats, 256) == hipSuccess) {
-    (void)hipMemsetAsync(dstats, 0, 256, st);
-    a.stats = dstats;
-  }
   tm.begin(NICE_PH_DEC_RECON, st);
   if (use_rows && rows_in_lds) {
     if (rows_lds > 64 * 1024)
@@ -524,6 +524,8 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
             "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
             "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
             h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
+    fprintf(stderr, "[nice dec stats] emit waves=%llu fills=%llu clk_fill=%llu clk_loop=%llu lane_syms=%llu\n",
+            h[20], h[18], h[16], h[17], h[19]);
     fprintf(stderr, "[nice dec stats] fix-up rounds per row: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5:%llu 6+:%llu\n",
             h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
     (void)hipFree(dstats);

@@ -188,33 +188,35 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
 // live in LDS; long codes (rare: longer than the LUT width) take a search over
 // the canonical order in global memory (L2-resident).
 // ---------------------------------------------------------------------------
-constexpr uint32_t RING_W = 24;        // words per lane ring
-constexpr uint32_t RING_STRIDE = 28;   // words between rings (16-byte aligned)
+constexpr uint32_t RING_W = 16;        // words per lane ring
+constexpr uint32_t RING_STRIDE = 20;   // words between rings (16-byte aligned)
 constexpr uint32_t RING_QUADS = RING_W / 4;
 
 struct LutLds {
   uint16_t lut[DEC_LUT_BUDGET];
-  uint32_t gp[16];   // per grammar state: lut_off | lut_bits << 16 | stream << 24
+  uint32_t lo[N_BINS];   // canonical order (long codes): aligned lower bounds,
+  uint16_t sym[N_BINS];  // symbols and lengths -- in LDS so a long code never
+  uint8_t len[N_BINS];   // waits on global memory (and on the lane's stores)
+  uint32_t gp[16];    // per grammar state: lut_off | lut_bits << 16 | max_aob << 24
+  uint32_t gs[16];    // per grammar state: canonical-order base | alphabet size << 16
 };
 
 __device__ inline void load_lut(LutLds& S, const DecTables* T) {
   const uint4* s = reinterpret_cast<const uint4*>(T->lut);
   uint4* d = reinterpret_cast<uint4*>(S.lut);
   for (uint32_t i = threadIdx.x; i < sizeof(S.lut) / 16; i += blockDim.x) d[i] = s[i];
+  for (uint32_t i = threadIdx.x; i < N_BINS; i += blockDim.x) {
+    S.lo[i] = T->lo[i];
+    S.sym[i] = T->sym[i];
+    S.len[i] = T->len[i];
+  }
   if (threadIdx.x < 13) {
     const int st = gs_stream((int)threadIdx.x);
-    S.gp[threadIdx.x] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) | ((uint32_t)st << 24);
+    S.gp[threadIdx.x] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) |
+                        ((uint32_t)T->max_aob[st] << 24);
+    S.gs[threadIdx.x] = (uint32_t)stream_base(st) | ((uint32_t)stream_size(st) << 16);
   }
 }
-
-struct Lane {
-  unsigned long long pos;   // absolute bit position in the frame's stream
-  uint32_t wi;              // window = words wi, wi + 1
-  uint32_t ws;              // word held in ring[0]
-  unsigned long long win;
-  uint32_t nxt;             // word wi + 2
-  bool ok;                  // nxt valid: one more symbol may be decoded
-};
 
 __device__ __forceinline__ uint32_t stream_word(const uint8_t* p, uint64_t len, uint32_t w) {
   uint32_t v = 0;
@@ -225,72 +227,91 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* p, uint64_t len, 
   return v;
 }
 
-// Wave-cooperative refill: every lane's ring restarts at its window word
-// (rounded down to 16 bytes).  Must be reached by all 64 lanes.
+// Lane bit reader over its LDS ring: a left-aligned 64-bit window (next bit at
+// bit 63) holding `avail` >= 32 valid bits between symbols.
+struct Lane {
+  unsigned long long pos;   // absolute bit position in the frame's stream
+  unsigned long long win;
+  uint32_t avail;
+  uint32_t rp;              // next ring word to shift in
+  bool ok;                  // the window can serve one more symbol
+};
+
+__device__ __forceinline__ void lane_seek(Lane& L, unsigned long long pos) {
+  L.pos = pos;
+  L.ok = false;
+}
+
+// Wave-cooperative refill: every lane's ring restarts at the word holding its
+// position (rounded down to 16 bytes).  Must be reached by all 64 lanes.
+__device__ __noinline__ void ring_fill_slow(uint32_t* dst, const uint8_t* p, uint64_t len, uint32_t w) {
+  dst[0] = stream_word(p, len, w);
+  dst[1] = stream_word(p, len, w + 1);
+  dst[2] = stream_word(p, len, w + 2);
+  dst[3] = stream_word(p, len, w + 3);
+}
 __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
                                           Lane& L) {
   const uint32_t lane = threadIdx.x & 63u;
-  L.ws = L.wi & ~3u;
+  const uint32_t ws = (uint32_t)(L.pos >> 5) & ~3u;
+  const uint64_t full_words = al16 ? (len >> 2) : 0;   // words fully inside the stream
 #pragma unroll
   for (uint32_t r = 0; r < RING_QUADS; ++r) {
     const uint32_t i = lane + 64u * r;
     const uint32_t owner = i / RING_QUADS, q = i - owner * RING_QUADS;
-    const uint32_t w = (uint32_t)__shfl((int)L.ws, (int)owner) + 4u * q;
-    uint4 v;
-    if (al16 && ((uint64_t)w + 4) * 4 <= len) {
-      v = *reinterpret_cast<const uint4*>(p + (uint64_t)w * 4);
+    const uint32_t w = (uint32_t)__shfl((int)ws, (int)owner) + 4u * q;
+    uint32_t* dst = wring + owner * RING_STRIDE + 4u * q;
+    if ((uint64_t)w + 4 <= full_words) {
+      uint4 v = *reinterpret_cast<const uint4*>(p + (uint64_t)w * 4);
       v.x = __builtin_bswap32(v.x); v.y = __builtin_bswap32(v.y);
       v.z = __builtin_bswap32(v.z); v.w = __builtin_bswap32(v.w);
+      *reinterpret_cast<uint4*>(dst) = v;
     } else {
-      v.x = stream_word(p, len, w); v.y = stream_word(p, len, w + 1);
-      v.z = stream_word(p, len, w + 2); v.w = stream_word(p, len, w + 3);
+      ring_fill_slow(dst, p, len, w);
     }
-    *reinterpret_cast<uint4*>(wring + owner * RING_STRIDE + 4u * q) = v;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   const uint32_t* my = wring + lane * RING_STRIDE;
-  const uint32_t o = L.wi - L.ws;
-  L.win = ((unsigned long long)my[o] << 32) | my[o + 1];
-  L.nxt = my[o + 2];
+  const uint32_t o = (uint32_t)(L.pos >> 5) - ws;
+  const uint32_t sh = (uint32_t)(L.pos & 31u);
+  L.win = (((unsigned long long)my[o] << 32) | my[o + 1]) << sh;
+  L.avail = 64u - sh;
+  L.rp = o + 2u;
   L.ok = true;
 }
 
-__device__ __forceinline__ void lane_seek(Lane& L, unsigned long long pos) {
-  L.pos = pos;
-  L.wi = (uint32_t)(pos >> 5);
-  L.ok = false;
+// Long code (longer than the LUT width): search of the canonical order.
+__device__ __forceinline__ uint32_t long_code(const LutLds& S, uint32_t v, uint32_t gp, uint32_t gsz) {
+  const uint32_t x = v >> (32u - (gp >> 24));
+  int lo = (int)(gsz & 0xFFFFu), hi = lo + (int)(gsz >> 16) - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (S.lo[mid] <= x) hi = mid;
+    else lo = mid + 1;
+  }
+  return ((uint32_t)S.sym[lo] << 5) | (uint32_t)S.len[lo];
 }
 
 // One symbol of grammar state g (requires L.ok).
-__device__ __forceinline__ uint32_t ring_symbol(Lane& L, const uint32_t* my, const LutLds& S,
-                                                const DecTables* T, uint32_t g) {
-  const uint32_t v = (uint32_t)((L.win << (L.pos & 31u)) >> 32);
+__device__ __forceinline__ uint32_t ring_symbol(Lane& L, const uint32_t* my, const LutLds& S, uint32_t g) {
+  const uint32_t v = (uint32_t)(L.win >> 32);
   const uint32_t gp = S.gp[g];
   const uint32_t lb = (gp >> 16) & 31u;
-  const uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - lb))];
-  uint32_t n = e & 31u, sym = e >> 5;
-  if (n == 0) {
-    const int s = (int)(gp >> 24);
-    const uint32_t x = v >> (32u - T->max_aob[s]);
-    int lo = stream_base(s), hi = stream_base(s) + stream_size(s) - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (T->lo[mid] <= x) hi = mid;
-      else lo = mid + 1;
-    }
-    n = T->len[lo];
-    sym = T->sym[lo];
-  }
+  uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - lb))];
+  if ((e & 31u) == 0) e = long_code(S, v, gp, S.gs[g]);
+  const uint32_t n = e & 31u, sym = e >> 5;
   L.pos += n;
-  if ((uint32_t)(L.pos >> 5) != L.wi) {   // codes are <= 31 bits: at most one word
-    ++L.wi;
-    L.win = (L.win << 32) | L.nxt;
-    const uint32_t o = L.wi + 2u - L.ws;
-    if (o < RING_W) L.nxt = my[o];
-    else L.ok = false;
-  }
+  L.win <<= n;
+  L.avail -= n;
+  // top up to >= 32 bits (branch-free: the ring read is always issued)
+  const uint32_t w = my[min(L.rp, RING_W - 1u)];
+  const bool need = L.avail < 32u;
+  L.ok = !(need && L.rp >= RING_W);
+  L.win |= need ? ((unsigned long long)w << (32u - L.avail)) : 0ull;
+  L.rp += need ? 1u : 0u;
+  L.avail += need ? 32u : 0u;
   return sym;
 }
 
@@ -298,26 +319,20 @@ __device__ __forceinline__ uint32_t ring_symbol(Lane& L, const uint32_t* my, con
 // read so far (kept in 1..64 once nonzero: the reference's u8 shift counter
 // `+= 3` only matters mod 64), px the pixels this symbol accounts for (run
 // digit d contributes d << 3k, plus the run's first pixel on its first digit).
+// Branch-free.
 constexpr uint32_t GS_FIRST = 1u | (2u << 4) | (5u << 8) | (9u << 12) | (10u << 16);
 constexpr uint32_t GS_LAST = (1u << 1) | (1u << 4) | (1u << 8) | (1u << 9) | (1u << 12);
 static_assert(P_BACK_REF == 0 && P_RGB == 1 && P_LUMA == 2 && P_SMALL_DIFF == 3 && P_LUMA2 == 4 &&
                   P_RUN1 == 5, "prefix numbering");
 
-__device__ __forceinline__ uint32_t gstep(uint32_t sym, uint32_t& g, uint32_t& dk, uint64_t& px) {
-  if (g == 0) {
-    if (sym >= (uint32_t)P_RUN1) {
-      const uint32_t d = sym - P_RUN1;
-      px += ((uint64_t)d << ((3u * dk) & 63u)) + (dk == 0 ? 1u : 0u);
-      dk = dk >= 64u ? 1u : dk + 1u;
-    } else {
-      px += 1;
-      dk = 0;
-      g = (GS_FIRST >> (4u * sym)) & 15u;
-    }
-  } else {
-    g = ((GS_LAST >> g) & 1u) ? 0u : g + 1u;
-  }
-  return sym;
+__device__ __forceinline__ void gstep(uint32_t sym, uint32_t& g, uint32_t& dk, uint64_t& px) {
+  const bool pre = g == 0;
+  const bool dig = pre && sym >= (uint32_t)P_RUN1;
+  const uint64_t runpx = ((uint64_t)(sym - P_RUN1) << ((3u * dk) & 63u)) + (dk == 0 ? 1u : 0u);
+  px += dig ? runpx : (pre ? 1u : 0u);
+  dk = dig ? (dk >= 64u ? 1u : dk + 1u) : (pre ? 0u : dk);
+  const uint32_t gn = ((GS_LAST >> g) & 1u) ? 0u : g + 1u;
+  g = pre ? (dig ? 0u : (GS_FIRST >> (4u * (sym & 7u))) & 15u) : gn;
 }
 
 // Packed parse state: bit position relative to the data start (40 bits),
@@ -395,20 +410,34 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   unsigned long long next_ck = begin + DEC_CK_BITS;
   unsigned long long ck_old = (check && nvalid_old > 0) ? ck[0] : ~0ull;
   bool active = need, synced = false;
-  while (__any(active)) {
-    ring_fill(wring, p, len, al16, L);
-    while (active && L.ok) {
-      if (L.pos >= end || L.pos >= hard || px > N) { active = false; break; }
-      gstep(ring_symbol(L, my, S, T, g), g, dk, px);
-      if (L.pos >= next_ck) {
-        const uint32_t cur = (uint32_t)(L.pos - begin) | (g << 16) | (dk << 20);
-        if (check && k < nvalid_old && (uint32_t)ck_old == cur) { synced = true; active = false; break; }
-        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)min(px, (uint64_t)0xFFFFFFFFu) << 32);
+  // Straight-line step: every lane decodes, only committing lanes keep the
+  // result (selects, no data-dependent control flow except checkpoints).
+  for (;;) {
+    const bool run = active && L.ok;
+    if (!__any(run)) {
+      if (!__any(active)) break;
+      ring_fill(wring, p, len, al16, L);
+      continue;
+    }
+    const bool stop = L.pos >= end || L.pos >= hard || px > N;
+    const bool commit = run && !stop;
+    Lane Ln = L;
+    uint32_t gn = g, dkn = dk;
+    uint64_t pxn = px;
+    gstep(ring_symbol(Ln, my, S, g), gn, dkn, pxn);
+    if (commit && Ln.pos >= next_ck) {   // checkpoint crossing (every ~128 bits)
+      const uint32_t cur = (uint32_t)(Ln.pos - begin) | (gn << 16) | (dkn << 20);
+      if (check && k < nvalid_old && (uint32_t)ck_old == cur) {
+        synced = true;
+      } else {
+        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)min(pxn, (uint64_t)0xFFFFFFFFu) << 32);
         ++k;
         next_ck = k < DEC_N_CK ? next_ck + DEC_CK_BITS : ~0ull;
         ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
       }
     }
+    if (commit) { L = Ln; g = gn; dk = dkn; px = pxn; }
+    if ((run && stop) || synced) active = false;
   }
   if (!need) return;
   if (synced) {
@@ -516,44 +545,40 @@ constexpr unsigned long long ID_CLS_PACK = [] {
   for (int id = 0; id < 16; ++id) v |= (unsigned long long)id_cls(id) << (4 * id);
   return v;
 }();
+constexpr uint32_t CLS_ROWS_PACK = [] {
+  uint32_t v = 0;
+  for (int c = 0; c < 16; ++c) v |= (uint32_t)cls_rows(c) << (2 * c);
+  return v;
+}();
+constexpr unsigned long long CLS_PX_PACK = [] {
+  unsigned long long v = 0;
+  for (int c = 0; c < 16; ++c) v |= (unsigned long long)(cls_px(c) + 3) << (3 * c);
+  return v;
+}();
 
-__device__ __forceinline__ int make_record(const DecArgs& a, uint64_t q, uint32_t mode, uint32_t s0,
-                                           uint32_t s1, uint32_t s2, uint32_t s3, uint32_t* rec) {
-  const uint64_t W = a.W;
-  switch (mode) {
-    case P_BACK_REF:
-    case P_LUMA: {
-      const uint32_t id = mode == P_BACK_REF ? s0 : 5u + s0;
-      if ((mode == P_BACK_REF && s0 >= 5) || (mode == P_LUMA && s0 >= 11)) return NICE_E_FORMAT;
-      const uint32_t cls = (uint32_t)(ID_CLS_PACK >> (4 * id)) & 15u;
-      const int64_t off = (int64_t)cls_rows((int)cls) * (int64_t)W + cls_px((int)cls);
-      // usize wrap (W < 3) or underflow before the image: the reference panics
-      if (off < 0 || (int64_t)q < off) return NICE_E_FORMAT;
-      uint32_t c = 0;
-      if (mode == P_LUMA) {
-        const uint32_t g = (s1 - 32u) & 255u;
-        c = ((s2 - 16u + g) & 255u) | (g << 8) | (((s3 - 16u + g) & 255u) << 16);
-      }
-      *rec = (cls << 24) | c;
-      return 0;
-    }
-    case P_SMALL_DIFF: {
-      const uint32_t rd = s0 % 7, t1 = s0 / 7;
-      *rec = ((rd - 3u) & 255u) | ((((t1 % 7) - 3u) & 255u) << 8) | ((((t1 / 7) - 3u) & 255u) << 16);
-      return 0;
-    }
-    case P_LUMA2: {
-      if (q < W) return NICE_E_FORMAT;   // position - channels*width underflows (code.rs:583)
-      const uint32_t g = (s0 - 32u) & 255u;
-      *rec = ((s1 - 16u + g) & 255u) | (g << 8) | (((s2 - 16u + g) & 255u) << 16);
-      return 0;
-    }
-    case P_RGB:
-      *rec = (s0 & 255u) | ((s1 & 255u) << 8) | ((s2 & 255u) << 16);
-      return 0;
-    default:
-      return NICE_E_FORMAT;
-  }
+
+// Record of a completed coded pixel (branch-free); `bad` when the reference
+// would panic on it (an index out of range or an offset before the image).
+__device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t mode, uint32_t s0,
+                                                uint32_t s1, uint32_t s2, uint32_t s3, bool& bad) {
+  const bool isbr = mode == P_BACK_REF, islu = mode == P_LUMA;
+  const bool issd = mode == P_SMALL_DIFF, isl2 = mode == P_LUMA2;
+  const uint32_t id = min(isbr ? s0 : 5u + s0, 15u);
+  const uint32_t cls = (uint32_t)(ID_CLS_PACK >> (4 * id)) & 15u;
+  const uint64_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
+  const int64_t off = (int64_t)(rows * W) + (int64_t)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;
+  // usize wrap (W < 3) or underflow before the image: the reference panics
+  const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0 >= 11u) || off < 0 || (int64_t)q < off;
+  const uint32_t gl = (s1 - 32u) & 255u;
+  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
+  const uint32_t rd = s0 % 7u, t1 = s0 / 7u;
+  const uint32_t c_sd = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
+  const uint32_t g2 = (s0 - 32u) & 255u;
+  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
+  const uint32_t c_rgb = (s0 & 255u) | ((s1 & 255u) << 8) | ((s2 & 255u) << 16);
+  // LUMA2 needs the row above: position - channels*width underflows (code.rs:583)
+  bad = (isbr || islu) ? bad_ref : (isl2 && q < W);
+  return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
 }
 
 struct RecGroup {
@@ -562,7 +587,8 @@ struct RecGroup {
   __device__ __forceinline__ void flush(uint32_t* rec, unsigned long long lo, unsigned long long hi) {
     if (!mask) return;
     if (grp >= lo && grp + 4 <= hi) {
-      *reinterpret_cast<uint4*>(rec + grp) = make_uint4(v0, v1, v2, v3);
+      uint4* dst = reinterpret_cast<uint4*>(__builtin_assume_aligned(rec + grp, 16));
+      *dst = make_uint4(v0, v1, v2, v3);
     } else {
       if (mask & 1u) rec[grp] = v0;
       if (mask & 2u) rec[grp + 1] = v1;
@@ -587,6 +613,11 @@ struct RecGroup {
     mask |= 1u << k;
   }
 };
+
+// payload slot of grammar state g: s0 for 1,2,5,9,10; s1 for 3,6,11; s2 for 4,7,12; s3 for 8
+constexpr uint32_t SLOT0 = (1u << 1) | (1u << 2) | (1u << 5) | (1u << 9) | (1u << 10);
+constexpr uint32_t SLOT1 = (1u << 3) | (1u << 6) | (1u << 11);
+constexpr uint32_t SLOT2 = (1u << 4) | (1u << 7) | (1u << 12);
 
 __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
   __shared__ LutLds S;
@@ -626,69 +657,68 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
   lane_seek(L, D + (e & ((1ull << 40) - 1)));
   uint32_t g = (uint32_t)(e >> 40) & 15u, dk = (uint32_t)(e >> 44) & 127u;
   // the pixel whose payload straddles our entry belongs to the previous chunk
-  bool straddle = true;
+  bool straddle = g != 0;
   bool closed = (q == N);          // a run completed exactly at N earlier
   uint32_t mode = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
   unsigned long long cur = 0;
-  int err = 0;
+  bool err = false;
   RecGroup G{~0ull, REC_RUN, REC_RUN, REC_RUN, REC_RUN, 0u};
-  while (__any(active)) {
-    ring_fill(wring, p, len, al16, L);
-    while (active && L.ok) {
-      if (L.pos >= hard) { active = false; break; }
-      uint64_t px = 0;
-      if (straddle) {
-        if (g == 0) { straddle = false; continue; }
-        gstep(ring_symbol(L, my, S, T, g), g, dk, px);
-        continue;
-      }
-      if (g == 0) {
-        if (q == N && (dk == 0 || closed)) {
-          // every pixel is accounted for; the reference still reads one more prefix
-          // (code.rs:660): a run digit there makes it copy past its buffer
-          if (strict) {
-            const uint32_t sym = gstep(ring_symbol(L, my, S, T, g), g, dk, px);
-            if (sym >= (uint32_t)P_RUN1) err = NICE_E_FORMAT;
-          }
-          active = false;
-          break;
-        }
-        if (L.pos >= end) { active = false; break; }   // next chunk continues from here
-      }
-      const uint32_t g0 = g, dk0 = dk;
-      const uint32_t sym = gstep(ring_symbol(L, my, S, T, g), g, dk, px);
-      if (g0 == 0) {
-        if (sym >= (uint32_t)P_RUN1) {      // run digit
-          if (q == N && dk0 == 0) {         // a digit right after the last pixel
-            if (strict) err = NICE_E_FORMAT;
-            active = false;
-            break;
-          }
-          q += px;
-          if (q > N) { err = NICE_E_FORMAT; active = false; break; }
-          if (q == N) closed = true;
-          continue;
-        }
-        closed = false;
-        mode = sym;
-        cur = q;
-        q += 1;
-        continue;
-      }
-      s0 = (g0 == 1 || g0 == 2 || g0 == 5 || g0 == 9 || g0 == 10) ? sym : s0;
-      s1 = (g0 == 3 || g0 == 6 || g0 == 11) ? sym : s1;
-      s2 = (g0 == 4 || g0 == 7 || g0 == 12) ? sym : s2;
-      s3 = (g0 == 8) ? sym : s3;
-      if (g == 0) {                          // payload complete
-        uint32_t r;
-        const int e2 = make_record(a, cur, mode, s0, s1, s2, s3, &r);
-        if (e2) { err = e2; active = false; break; }
-        G.put(rec, q0, cur, r);
-      }
+  for (;;) {
+    const bool run = active && L.ok;
+    if (!__any(run)) {
+      if (!__any(active)) break;
+      ring_fill(wring, p, len, al16, L);
+      continue;
     }
+    // decode one symbol on every lane; commit where the lane's state allows
+    const uint32_t g0 = g, dk0 = dk;
+    Lane Ln = L;
+    const uint32_t sym = ring_symbol(Ln, my, S, g0);
+    uint32_t gn = g0, dkn = dk0;
+    uint64_t px = 0;
+    gstep(sym, gn, dkn, px);
+    const bool pre = g0 == 0;
+    const bool dig = pre && sym >= (uint32_t)P_RUN1;
+    const bool atpre = !straddle && pre;
+    // every pixel accounted for: the reference still reads one more prefix
+    // (code.rs:660); a run digit there makes it copy past its buffer
+    const bool stop_n = atpre && q == N && (dk0 == 0 || closed);
+    const bool stop_end = atpre && !stop_n && L.pos >= end;   // next chunk continues here
+    const bool stop_hard = L.pos >= hard;
+    err = err || (run && stop_n && !stop_hard && strict && dig);
+    const bool commit = run && !stop_n && !stop_end && !stop_hard;
+    const bool own = commit && !straddle;      // the symbol belongs to this chunk's pixels
+    const bool newpx = own && pre && !dig;
+    const unsigned long long qn = q + ((own && dig) ? px : 0ull);
+    cur = newpx ? qn : cur;
+    mode = newpx ? sym : mode;
+    closed = (own && dig) ? (closed || qn == N) : (newpx ? false : closed);
+    const unsigned long long q2 = qn + (newpx ? 1ull : 0ull);
+    const bool over = own && q2 > N;
+    if (own && !pre) {
+      s0 = ((SLOT0 >> g0) & 1u) ? sym : s0;
+      s1 = ((SLOT1 >> g0) & 1u) ? sym : s1;
+      s2 = ((SLOT2 >> g0) & 1u) ? sym : s2;
+      s3 = g0 == 8u ? sym : s3;
+    }
+    if (own && !pre && gn == 0) {            // payload complete: the record
+      bool bad;
+      const uint32_t r = make_record(a.W, cur, mode, s0, s1, s2, s3, bad);
+      if (bad) err = true;
+      else G.put(rec, q0, cur, r);
+    }
+    if (commit) {
+      L = Ln;
+      g = gn;
+      dk = dkn;
+      q = q2;
+      straddle = straddle && gn != 0;
+    }
+    if ((run && !commit) || over || err) active = false;
+    err = err || over;
   }
   G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
-  if (err) set_status(&a.status[f], err);
+  if (err) set_status(&a.status[f], NICE_E_FORMAT);
 }
 
 // ---------------------------------------------------------------------------
@@ -936,17 +966,6 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
 // ---------------------------------------------------------------------------
 constexpr int ROWS_SEG = 16;
 constexpr uint32_t ROWS_RING = 4;   // rows y-4 .. y-1 while row y is built
-
-constexpr uint32_t CLS_ROWS_PACK = [] {
-  uint32_t v = 0;
-  for (int c = 0; c < 16; ++c) v |= (uint32_t)cls_rows(c) << (2 * c);
-  return v;
-}();
-constexpr unsigned long long CLS_PX_PACK = [] {
-  unsigned long long v = 0;
-  for (int c = 0; c < 16; ++c) v |= (unsigned long long)(cls_px(c) + 3) << (3 * c);
-  return v;
-}();
 
 // Per-pixel word: spread constant c in the field bits, the kind as one-hot
 // flags in the guard bits -- W_L1/W_L2/W_L3: c plus the pixel 1..3 back;
