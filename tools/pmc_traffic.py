@@ -20,7 +20,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = re.split(r"[(<]", r["Kernel_Name"])[0].strip()
+        name = re.split(r"[(<]", r["Kernel_Name"])[0].strip().replace("nice::", "")
         if name.startswith("__amd") or not name:
             continue
         acc[name].append(float(r["Counter_Value"]))
