@@ -63,6 +63,37 @@ __device__ inline void stage_tile(TileWin& tw, const uint8_t* __restrict__ frame
   }
 }
 
+// Software-pipelined staging for 4-byte pixels: raw words of the next tile are
+// loaded into registers while the current tile is classified, then spread
+// into the LDS windows.
+constexpr int STAGE_PER_THREAD = (WIN + ENC_THREADS - 1) / ENC_THREADS;   // 5
+struct TilePrefetch {
+  uint32_t v[4][STAGE_PER_THREAD];
+};
+__device__ __forceinline__ void prefetch_tile(TilePrefetch& pf, const uint8_t* __restrict__ frame,
+                                              int64_t start, int64_t N, uint32_t W) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t base = start - (int64_t)k * W - 3;
+#pragma unroll
+    for (int i = 0; i < STAGE_PER_THREAD; ++i) {
+      const int j = (int)threadIdx.x + i * ENC_THREADS;
+      const int64_t g = base + j;
+      pf.v[k][i] = (j < WIN && g >= 0 && g < N) ? reinterpret_cast<const uint32_t*>(frame)[g] : 0u;
+    }
+  }
+}
+__device__ __forceinline__ void commit_tile(TileWin& tw, const TilePrefetch& pf) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int i = 0; i < STAGE_PER_THREAD; ++i) {
+      const int j = (int)threadIdx.x + i * ENC_THREADS;
+      if (j < WIN) tw.w[k][j] = spread_rgba(pf.v[k][i]);
+    }
+  }
+}
+
 struct WinAcc {
   const TileWin* tw;
   int col;  // p + 3
@@ -185,6 +216,14 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) hist[b] = 0;
   uint32_t cur_frame = (uint32_t)(t_begin / a.tiles_per_frame);
   const int lane = threadIdx.x & 63;
+  const int64_t N = (int64_t)a.W * a.H;
+  const bool rgba = a.C == 4;
+  TilePrefetch pf;
+  if (rgba) {
+    const uint32_t f0 = (uint32_t)(t_begin / a.tiles_per_frame);
+    prefetch_tile(pf, a.px + (uint64_t)f0 * a.frame_stride,
+                  (int64_t)(t_begin % a.tiles_per_frame) * ENC_TILE, N, a.W);
+  }
 
   for (uint64_t t = t_begin; t < t_end; ++t) {
     const uint32_t f = (uint32_t)(t / a.tiles_per_frame);
@@ -199,10 +238,18 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
     }
     const uint8_t* frame = a.px + (uint64_t)f * a.frame_stride;
     const int64_t start = (int64_t)tt * ENC_TILE;
-    const int64_t N = (int64_t)a.W * a.H;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
     __syncthreads();
-    stage_tile(tw, frame, start, N, a.W, a.C);
+    if (rgba) {
+      commit_tile(tw, pf);
+      if (t + 1 < t_end) {   // next tile's pixels are in flight while this one is classified
+        const uint32_t f1 = (uint32_t)((t + 1) / a.tiles_per_frame);
+        prefetch_tile(pf, a.px + (uint64_t)f1 * a.frame_stride,
+                      (int64_t)((t + 1) % a.tiles_per_frame) * ENC_TILE, N, a.W);
+      }
+    } else {
+      stage_tile(tw, frame, start, N, a.W, a.C);
+    }
     __syncthreads();
 
     // coded flags -> bitmask
