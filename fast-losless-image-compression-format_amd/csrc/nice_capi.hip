@@ -306,7 +306,7 @@ struct DecLayout {
   size_t total;
   size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
 };
-DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint64_t npx, size_t rowbuf) {
+DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf) {
   DecLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -314,7 +314,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint64_t npx, size_
   L.o_dstart = take((size_t)n_frames * 8);
   L.o_entry = take((size_t)n_frames * max_chunks * 8);
   L.o_last = take((size_t)n_frames * max_chunks * 8);
-  L.o_ck = take((size_t)n_frames * DEC_N_CK * max_chunks * 8);
+  L.o_ck = take((size_t)n_frames * n_ck * max_chunks * 8);
   L.o_cpx = take((size_t)n_frames * max_chunks * 8);
   L.o_cstart = take((size_t)n_frames * max_chunks * 8);
   L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
@@ -420,8 +420,20 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
     max_len = l > max_len ? l : max_len;
   }
   const uint64_t D = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
-  const uint32_t max_chunks =
-      max_len * 8 > D ? (uint32_t)((max_len * 8 - D + DEC_CHUNK_BITS - 1) / DEC_CHUNK_BITS) : 1;
+  // slice size: long slices make the Jacobi re-parses (which run until the
+  // slowest lane of a wave re-synchronises, ~1000 bits) cheap relative to the
+  // first pass, short ones keep a small batch filling the GPU: aim for about
+  // 256 CUs x 8 waves x 64 lanes x 2 slices, as a power of two in [1K, 16K]
+  uint64_t total_bits = 0;
+  for (uint64_t l : lens) total_bits += l * 8 > D ? l * 8 - D : 0;
+  uint32_t cb = DEC_MIN_CHUNK_BITS;
+  while (cb < DEC_MAX_CHUNK_BITS && total_bits / (2ull * cb) > 256ull * 8 * 64 * 2) cb *= 2;
+  if (const char* ev = getenv("NICE_DEC_SLICE_BITS")) {   // tests: force a slice size
+    const uint32_t v = (uint32_t)atoi(ev);
+    if (v >= DEC_MIN_CHUNK_BITS && v <= DEC_MAX_CHUNK_BITS && (v & (v - 1)) == 0) cb = v;
+  }
+  const uint32_t max_chunks = max_len * 8 > D ? (uint32_t)((max_len * 8 - D + cb - 1) / cb) : 1;
+  const uint32_t n_ck = cb / DEC_CK_BITS - 1;
   const RecGeom g = rec_geom(w);
   // multi-wave row kernel for 64 <= W <= 16384 (one lane per 16-pixel segment),
   // single-wave kernel otherwise
@@ -431,7 +443,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
   const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * w * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
-  DecLayout L = dec_layout(n_frames, max_chunks, N, rowbuf);
+  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf);
   int rc = ctx->dec.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->dec.ptr;
@@ -450,6 +462,9 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   a.tables = base + L.o_tables;
   a.data_start = (unsigned long long*)(base + L.o_dstart);
   a.max_chunks = max_chunks;
+  a.chunk_bits = cb;
+  a.n_ck = n_ck;
+  a.emit_blocks = (uint32_t)(((uint64_t)max_chunks * (cb / DEC_EMIT_BITS) + 255) / 256);
   a.chunk_blocks = (max_chunks + 255) / 256;
   a.chunk_px = (unsigned long long*)(base + L.o_cpx);
   a.chunk_start = (unsigned long long*)(base + L.o_cstart);
@@ -472,6 +487,12 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
     NICE_HIP(hipGetLastError());
     return NICE_OK;
   }
+  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
+  unsigned long long* dstats = nullptr;
+  if (want_stats && hipMalloc(&dstats, 512) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 512, st);
+    a.stats = dstats;
+  }
   hipLaunchKernelGGL(dec_init_entries, dim3((max_chunks + 255) / 256 < 64 ? (max_chunks + 255) / 256 : 64, n_frames),
                      dim3(256), 0, st, a);
   const dim3 cgrid(n_frames * a.chunk_blocks);
@@ -490,15 +511,9 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
-  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
-  unsigned long long* dstats = nullptr;
-  if (want_stats && hipMalloc(&dstats, 256) == hipSuccess) {
-    (void)hipMemsetAsync(dstats, 0, 256, st);
-    a.stats = dstats;
-  }
   tm.begin(NICE_PH_DEC_EMIT, st);
   NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
-  hipLaunchKernelGGL(dec_emit, cgrid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dec_emit, dim3(n_frames * a.emit_blocks), dim3(256), 0, st, a);
   tm.end(st);
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
@@ -516,16 +531,19 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   }
   tm.end(st);
   if (dstats) {
-    unsigned long long h[32] = {0};
-    (void)hipMemcpyAsync(h, dstats, 256, hipMemcpyDeviceToHost, st);
+    unsigned long long h[64] = {0};
+    (void)hipMemcpyAsync(h, dstats, 512, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
             "[nice dec stats] rows=%llu unconverged_segs=%llu tail_unknown_segs=%llu "
             "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
             "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
             h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
-    fprintf(stderr, "[nice dec stats] emit waves=%llu fills=%llu clk_fill=%llu clk_loop=%llu lane_syms=%llu\n",
-            h[20], h[18], h[16], h[17], h[19]);
+    fprintf(stderr, "[nice dec stats] re-parse met previous parse at checkpoint:");
+    for (int k = 0; k < 17; ++k) fprintf(stderr, " %d:%llu", k, h[32 + k]);
+    fprintf(stderr, "\n");
+    fprintf(stderr, "[nice dec stats] slice=%u emit waves=%llu wave_iters=%llu active_lane_iters=%llu fills=%llu\n",
+            a.chunk_bits, h[20], h[16], h[17], h[18]);
     fprintf(stderr, "[nice dec stats] fix-up rounds per row: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5:%llu 6+:%llu\n",
             h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
     (void)hipFree(dstats);

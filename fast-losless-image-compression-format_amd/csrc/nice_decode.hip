@@ -180,25 +180,30 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
 // ---------------------------------------------------------------------------
 // Parse machinery shared by dec_sync and dec_emit.
 //
-// One lane per 2048-bit chunk, 64 consecutive chunks per wave.  A lane reads
-// its bits from a private ring of RING_W big-endian words in LDS; the wave
-// refills all 64 rings together with 16-byte loads (consecutive lanes load
-// consecutive 16 bytes of one ring), so the stream is read from HBM in whole
-// lines instead of one 4-byte word per lane per load.  The first-level LUTs
-// live in LDS; long codes (rare: longer than the LUT width) take a search over
-// the canonical order in global memory (L2-resident).
+// A lane parses one slice of the data bits.  It reads them from a private ring
+// of RING_W big-endian words in LDS, refilled for the whole wave at once with
+// 16-byte loads (consecutive lanes load consecutive 16 bytes of one ring), so
+// the stream is read from HBM in whole lines.  The first-level LUTs and the
+// canonical order for long codes live in LDS.
+//
+// The parse advances one pixel event per step: a prefix symbol, then -- for a
+// coded pixel -- the mode's fixed payload sequence (code.rs:576-644): BACK_REF
+// k; RGB r g b; LUMA ref, g, r, b; SMALL_DIFF index; LUMA2 g r b.  Slices
+// therefore begin and end at prefix positions: a slice's parse stops at the
+// first prefix at or after its end bit, which is where the next slice starts.
 // ---------------------------------------------------------------------------
-constexpr uint32_t RING_W = 16;        // words per lane ring
-constexpr uint32_t RING_STRIDE = 20;   // words between rings (16-byte aligned)
+constexpr uint32_t RING_W = 20;        // words per lane ring
+constexpr uint32_t RING_STRIDE = 20;   // 80 bytes: 16-byte aligned rings
 constexpr uint32_t RING_QUADS = RING_W / 4;
+constexpr uint32_t PIXEL_WORDS = 5;    // one pixel event: <= 5 symbols of <= 31 bits
 
 struct LutLds {
   uint16_t lut[DEC_LUT_BUDGET];
   uint32_t lo[N_BINS];   // canonical order (long codes): aligned lower bounds,
-  uint16_t sym[N_BINS];  // symbols and lengths -- in LDS so a long code never
-  uint8_t len[N_BINS];   // waits on global memory (and on the lane's stores)
-  uint32_t gp[16];    // per grammar state: lut_off | lut_bits << 16 | max_aob << 24
-  uint32_t gs[16];    // per grammar state: canonical-order base | alphabet size << 16
+  uint16_t sym[N_BINS];  // symbols and lengths
+  uint8_t len[N_BINS];
+  uint32_t gp[16];    // per stream: lut_off | lut_bits << 16 | max_aob << 24
+  uint32_t gs[16];    // per stream: canonical-order base | alphabet size << 16
 };
 
 __device__ inline void load_lut(LutLds& S, const DecTables* T) {
@@ -210,11 +215,10 @@ __device__ inline void load_lut(LutLds& S, const DecTables* T) {
     S.sym[i] = T->sym[i];
     S.len[i] = T->len[i];
   }
-  if (threadIdx.x < 13) {
-    const int st = gs_stream((int)threadIdx.x);
-    S.gp[threadIdx.x] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) |
-                        ((uint32_t)T->max_aob[st] << 24);
-    S.gs[threadIdx.x] = (uint32_t)stream_base(st) | ((uint32_t)stream_size(st) << 16);
+  if (threadIdx.x < N_STREAMS) {
+    const int st = (int)threadIdx.x;
+    S.gp[st] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) | ((uint32_t)T->max_aob[st] << 24);
+    S.gs[st] = (uint32_t)stream_base(st) | ((uint32_t)stream_size(st) << 16);
   }
 }
 
@@ -234,40 +238,43 @@ struct Lane {
   unsigned long long win;
   uint32_t avail;
   uint32_t rp;              // next ring word to shift in
-  bool ok;                  // the window can serve one more symbol
 };
+// one more pixel event fits in the ring
+__device__ __forceinline__ bool lane_ok(const Lane& L) { return L.rp + PIXEL_WORDS <= RING_W; }
 
-__device__ __forceinline__ void lane_seek(Lane& L, unsigned long long pos) {
-  L.pos = pos;
-  L.ok = false;
-}
-
-// Wave-cooperative refill: every lane's ring restarts at the word holding its
-// position (rounded down to 16 bytes).  Must be reached by all 64 lanes.
 __device__ __noinline__ void ring_fill_slow(uint32_t* dst, const uint8_t* p, uint64_t len, uint32_t w) {
   dst[0] = stream_word(p, len, w);
   dst[1] = stream_word(p, len, w + 1);
   dst[2] = stream_word(p, len, w + 2);
   dst[3] = stream_word(p, len, w + 3);
 }
+// Wave-cooperative refill: every lane's ring restarts at the word holding its
+// position (rounded down to 16 bytes).  Must be reached by all 64 lanes.
 __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
                                           Lane& L) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t ws = (uint32_t)(L.pos >> 5) & ~3u;
   const uint64_t full_words = al16 ? (len >> 2) : 0;   // words fully inside the stream
+  uint4 v[RING_QUADS];
+  uint32_t wq[RING_QUADS];
+#pragma unroll
+  for (uint32_t r = 0; r < RING_QUADS; ++r) {   // issue every load before waiting on any
+    const uint32_t i = lane + 64u * r;
+    const uint32_t owner = i / RING_QUADS, q = i - owner * RING_QUADS;
+    wq[r] = (uint32_t)__shfl((int)ws, (int)owner) + 4u * q;   // all lanes: before any branch
+    const uint64_t wl = (uint64_t)wq[r] + 4 <= full_words ? wq[r] : 0u;
+    v[r] = *reinterpret_cast<const uint4*>(p + wl * 4);
+  }
 #pragma unroll
   for (uint32_t r = 0; r < RING_QUADS; ++r) {
     const uint32_t i = lane + 64u * r;
     const uint32_t owner = i / RING_QUADS, q = i - owner * RING_QUADS;
-    const uint32_t w = (uint32_t)__shfl((int)ws, (int)owner) + 4u * q;
     uint32_t* dst = wring + owner * RING_STRIDE + 4u * q;
-    if ((uint64_t)w + 4 <= full_words) {
-      uint4 v = *reinterpret_cast<const uint4*>(p + (uint64_t)w * 4);
-      v.x = __builtin_bswap32(v.x); v.y = __builtin_bswap32(v.y);
-      v.z = __builtin_bswap32(v.z); v.w = __builtin_bswap32(v.w);
-      *reinterpret_cast<uint4*>(dst) = v;
+    if ((uint64_t)wq[r] + 4 <= full_words) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(__builtin_bswap32(v[r].x), __builtin_bswap32(v[r].y),
+                                                  __builtin_bswap32(v[r].z), __builtin_bswap32(v[r].w));
     } else {
-      ring_fill_slow(dst, p, len, w);
+      ring_fill_slow(dst, p, len, wq[r]);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -279,7 +286,6 @@ __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uin
   L.win = (((unsigned long long)my[o] << 32) | my[o + 1]) << sh;
   L.avail = 64u - sh;
   L.rp = o + 2u;
-  L.ok = true;
 }
 
 // Long code (longer than the LUT width): search of the canonical order.
@@ -294,78 +300,101 @@ __device__ __forceinline__ uint32_t long_code(const LutLds& S, uint32_t v, uint3
   return ((uint32_t)S.sym[lo] << 5) | (uint32_t)S.len[lo];
 }
 
-// One symbol of grammar state g (requires L.ok).
-__device__ __forceinline__ uint32_t ring_symbol(Lane& L, const uint32_t* my, const LutLds& S, uint32_t g) {
+// One symbol of stream st.
+__device__ __forceinline__ uint32_t dsym(Lane& L, const uint32_t* my, const LutLds& S, uint32_t st) {
   const uint32_t v = (uint32_t)(L.win >> 32);
-  const uint32_t gp = S.gp[g];
-  const uint32_t lb = (gp >> 16) & 31u;
-  uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - lb))];
-  if ((e & 31u) == 0) e = long_code(S, v, gp, S.gs[g]);
-  const uint32_t n = e & 31u, sym = e >> 5;
+  const uint32_t gp = S.gp[st];
+  uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - ((gp >> 16) & 31u)))];
+  if ((e & 31u) == 0) e = long_code(S, v, gp, S.gs[st]);
+  const uint32_t n = e & 31u;
   L.pos += n;
   L.win <<= n;
   L.avail -= n;
-  // top up to >= 32 bits (branch-free: the ring read is always issued)
+  // top up to >= 32 bits (branch-free; lane_ok() guarantees the word exists)
   const uint32_t w = my[min(L.rp, RING_W - 1u)];
   const bool need = L.avail < 32u;
-  L.ok = !(need && L.rp >= RING_W);
   L.win |= need ? ((unsigned long long)w << (32u - L.avail)) : 0ull;
   L.rp += need ? 1u : 0u;
   L.avail += need ? 32u : 0u;
-  return sym;
+  return e >> 5;
 }
-
-// Grammar step (code.rs:576-671): g is the grammar state, dk the run digits
-// read so far (kept in 1..64 once nonzero: the reference's u8 shift counter
-// `+= 3` only matters mod 64), px the pixels this symbol accounts for (run
-// digit d contributes d << 3k, plus the run's first pixel on its first digit).
-// Branch-free.
-constexpr uint32_t GS_FIRST = 1u | (2u << 4) | (5u << 8) | (9u << 12) | (10u << 16);
-constexpr uint32_t GS_LAST = (1u << 1) | (1u << 4) | (1u << 8) | (1u << 9) | (1u << 12);
+constexpr uint32_t PFX_STREAM = S_PREFIX;
+// payload stream i of mode m (code.rs:576-644), 4 bits each at 4 * (4m + i)
+constexpr unsigned long long PAY_STREAMS =
+    ((unsigned long long)S_BACK_REF << 0) |
+    ((unsigned long long)S_RGB << 16) | ((unsigned long long)S_RGB << 20) | ((unsigned long long)S_RGB << 24) |
+    ((unsigned long long)S_LUMA_REF << 32) | ((unsigned long long)S_LUMA_BASE << 36) |
+    ((unsigned long long)S_LUMA_OTHER << 40) | ((unsigned long long)S_LUMA_OTHER << 44) |
+    ((unsigned long long)S_SMALL_DIFF << 48);   // mode 4 (LUMA2): pay_stream
 static_assert(P_BACK_REF == 0 && P_RGB == 1 && P_LUMA == 2 && P_SMALL_DIFF == 3 && P_LUMA2 == 4 &&
                   P_RUN1 == 5, "prefix numbering");
-
-__device__ __forceinline__ void gstep(uint32_t sym, uint32_t& g, uint32_t& dk, uint64_t& px) {
-  const bool pre = g == 0;
-  const bool dig = pre && sym >= (uint32_t)P_RUN1;
-  const uint64_t runpx = ((uint64_t)(sym - P_RUN1) << ((3u * dk) & 63u)) + (dk == 0 ? 1u : 0u);
-  px += dig ? runpx : (pre ? 1u : 0u);
-  dk = dig ? (dk >= 64u ? 1u : dk + 1u) : (pre ? 0u : dk);
-  const uint32_t gn = ((GS_LAST >> g) & 1u) ? 0u : g + 1u;
-  g = pre ? (dig ? 0u : (GS_FIRST >> (4u * (sym & 7u))) & 15u) : gn;
+__device__ __forceinline__ uint32_t pay_stream(uint32_t m, uint32_t i) {
+  // mode 4 (LUMA2) does not fit the 64-bit table: handled here
+  return m == (uint32_t)P_LUMA2 ? (uint32_t)S_LUMA2_BASE + i : (uint32_t)(PAY_STREAMS >> (4u * (4u * m + i))) & 15u;
 }
 
-// Packed parse state: bit position relative to the data start (40 bits),
-// grammar state (4), run digits (7).  Bits 56..63 of `last` hold the number of
-// valid checkpoints.
+// One pixel event at a prefix position: the prefix and, for a coded pixel, its
+// payload symbols.  Returns the prefix; s0..s3 receive the payload.
+__device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, const LutLds& S, uint32_t& s0,
+                                                uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+  const uint32_t pfx = dsym(L, my, S, PFX_STREAM);
+  if (pfx < (uint32_t)P_RUN1) {
+    s0 = dsym(L, my, S, pay_stream(pfx, 0));
+    if (pfx == (uint32_t)P_RGB || pfx == (uint32_t)P_LUMA || pfx == (uint32_t)P_LUMA2) {
+      s1 = dsym(L, my, S, pay_stream(pfx, 1));
+      s2 = dsym(L, my, S, pay_stream(pfx, 2));
+      if (pfx == (uint32_t)P_LUMA) s3 = dsym(L, my, S, S_LUMA_OTHER);
+    }
+  }
+  return pfx;
+}
+
+// Pixels a prefix accounts for: 1 for a coded pixel; a run digit d contributes
+// d << 3k (k = digits read before it; the reference's u8 shift counter `+= 3`
+// only matters mod 64) plus the run's first pixel on its first digit
+// (code.rs:660-680).  dk: digits read in the current run, kept in 1..64 once
+// nonzero.  Saturates at 2^32 - 1 (only garbage parses get there).
+__device__ __forceinline__ uint32_t pixel_count(uint32_t pfx, uint32_t& dk) {
+  if (pfx < (uint32_t)P_RUN1) { dk = 0; return 1u; }
+  const uint32_t sh = (3u * dk) & 63u;
+  const uint64_t c = ((uint64_t)(pfx - P_RUN1) << sh) + (dk == 0 ? 1u : 0u);
+  dk = dk >= 64u ? 1u : dk + 1u;
+  return c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
+}
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) { return a + b < a ? 0xFFFFFFFFu : a + b; }
+
+// Packed slice entry: bit position relative to the data start (40 bits), run
+// digits read so far (7).  Bits 56..63 of `last` hold the number of valid
+// checkpoints.  Checkpoint: position in the slice (16), run digits (7) << 20,
+// pixels since the slice entry << 32.
 constexpr unsigned long long PS_MASK = (1ull << 51) - 1ull;
-__device__ __forceinline__ unsigned long long ps_pack(unsigned long long rel, uint32_t g, uint32_t dk) {
-  return rel | ((unsigned long long)g << 40) | ((unsigned long long)dk << 44);
+__device__ __forceinline__ unsigned long long ps_pack(unsigned long long rel, uint32_t dk) {
+  return rel | ((unsigned long long)dk << 44);
 }
 
 // chunk geometry: chunk j of frame f covers bits [D + j*CB, D + (j+1)*CB)
-__device__ __forceinline__ uint32_t n_chunks(uint64_t len, uint64_t D) {
+__device__ __forceinline__ uint32_t n_chunks(uint64_t len, uint64_t D, uint32_t cb) {
   const uint64_t bits = len * 8;
-  return bits > D ? (uint32_t)((bits - D + DEC_CHUNK_BITS - 1) / DEC_CHUNK_BITS) : 0u;
+  return bits > D ? (uint32_t)((bits - D + cb - 1) / cb) : 0u;
 }
 
-// Initial entry guesses: every chunk starts at its first bit expecting a prefix.
+// Initial entry guesses: every slice starts at its first bit, at a prefix.
 __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
   const uint32_t f = blockIdx.y;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < a.max_chunks; j += gridDim.x * 256) {
     const uint64_t i = (uint64_t)f * a.max_chunks + j;
-    a.entry[i] = ps_pack((unsigned long long)j * DEC_CHUNK_BITS, 0, 0);
+    a.entry[i] = ps_pack((unsigned long long)j * a.chunk_bits, 0);
     a.last[i] = ~0ull;
   }
 }
 
 // ---------------------------------------------------------------------------
-// D1: sync iteration (Jacobi, in place).  Each lane parses its chunk from the
-// current entry guess and writes the exit as the next chunk's entry.  Lanes
+// D1: sync iteration (Jacobi, in place).  Each lane parses its slice from the
+// current entry guess and writes the exit as the next slice's entry.  Lanes
 // whose entry did not change since their last parse do nothing.  A re-parse
-// compares its state with the previous parse at every CK_BITS checkpoint; once
-// they agree the rest of the chunk is unchanged (Huffman self-synchronisation),
-// so the lane stops and only patches its pixel count.
+// compares its state with the previous parse at the first prefix after every
+// CK_BITS; once they agree the rest of the slice is unchanged (Huffman
+// self-synchronisation), so the lane stops and only patches its pixel count.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   __shared__ LutLds S;
@@ -375,7 +404,7 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   if (a.status[f] != 0) return;
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
-  const uint32_t nc = n_chunks(len, D);
+  const uint32_t nc = n_chunks(len, D, a.chunk_bits);
   if (jb * 256u >= nc) return;
   const uint32_t j = jb * 256u + threadIdx.x;
   const uint64_t base = (uint64_t)f * a.max_chunks;
@@ -386,8 +415,7 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   }
   const bool need = j < nc && (last == ~0ull || (last & PS_MASK) != e);
   if (!__syncthreads_or(need)) return;
-  const DecTables* T = reinterpret_cast<const DecTables*>(a.tables) + f;
-  load_lut(S, T);
+  load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
   if (jb * 256u + wave * 64u >= nc) return;
@@ -397,52 +425,49 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   const bool check = last != ~0ull;
   const uint32_t nvalid_old = (uint32_t)(last >> 56);
-  const unsigned long long begin = D + (unsigned long long)j * DEC_CHUNK_BITS;
-  const unsigned long long end = begin + DEC_CHUNK_BITS;
+  const unsigned long long begin = D + (unsigned long long)j * a.chunk_bits;
+  const unsigned long long end = begin + a.chunk_bits;
   const unsigned long long hard = len * 8 + 64;
-  const uint64_t N = (uint64_t)a.W * a.H;
-  unsigned long long* ck = a.ck + (uint64_t)f * DEC_N_CK * a.max_chunks + j;
+  const uint32_t N = a.W * a.H;
+  unsigned long long* ck = a.ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
   Lane L;
-  lane_seek(L, D + (e & ((1ull << 40) - 1)));
-  uint32_t g = (uint32_t)(e >> 40) & 15u, dk = (uint32_t)(e >> 44) & 127u;
-  uint64_t px = 0;
-  uint32_t k = 0;
+  L.pos = D + (e & ((1ull << 40) - 1));
+  L.rp = RING_W;   // empty: filled on the first step
+  uint32_t dk = (uint32_t)(e >> 44) & 127u;
+  uint32_t px = 0, k = 0;
   unsigned long long next_ck = begin + DEC_CK_BITS;
   unsigned long long ck_old = (check && nvalid_old > 0) ? ck[0] : ~0ull;
   bool active = need, synced = false;
-  // Straight-line step: every lane decodes, only committing lanes keep the
-  // result (selects, no data-dependent control flow except checkpoints).
   for (;;) {
-    const bool run = active && L.ok;
-    if (!__any(run)) {
-      if (!__any(active)) break;
-      ring_fill(wring, p, len, al16, L);
-      continue;
-    }
-    const bool stop = L.pos >= end || L.pos >= hard || px > N;
-    const bool commit = run && !stop;
-    Lane Ln = L;
-    uint32_t gn = g, dkn = dk;
-    uint64_t pxn = px;
-    gstep(ring_symbol(Ln, my, S, g), gn, dkn, pxn);
-    if (commit && Ln.pos >= next_ck) {   // checkpoint crossing (every ~128 bits)
-      const uint32_t cur = (uint32_t)(Ln.pos - begin) | (gn << 16) | (dkn << 20);
+    // at a prefix position: slice end, checkpoint, or one more pixel event
+    if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
+    if (active && L.pos >= next_ck) {
+      const uint32_t cur = (uint32_t)(L.pos - begin) | (dk << 20);
       if (check && k < nvalid_old && (uint32_t)ck_old == cur) {
         synced = true;
+        active = false;
       } else {
-        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)min(pxn, (uint64_t)0xFFFFFFFFu) << 32);
+        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
         ++k;
-        next_ck = k < DEC_N_CK ? next_ck + DEC_CK_BITS : ~0ull;
+        next_ck = k < a.n_ck ? next_ck + DEC_CK_BITS : ~0ull;
         ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
       }
     }
-    if (commit) { L = Ln; g = gn; dk = dkn; px = pxn; }
-    if ((run && stop) || synced) active = false;
+    if (!__any(active)) break;
+    if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
+    if (active) {
+      uint32_t s0, s1, s2, s3;
+      const uint32_t pfx = pixel_event(L, my, S, s0, s1, s2, s3);
+      px = sat_add(px, pixel_count(pfx, dk));
+    }
   }
   if (!need) return;
+  if (a.stats && check) {   // diagnostics: where re-parses met the previous parse (16: never)
+    atomicAdd(&a.stats[32 + (synced ? min(k, 15u) : 16u)], 1ull);
+  }
   if (synced) {
     // from checkpoint k on this parse equals the previous one, shifted by delta pixels
-    const uint32_t delta = (uint32_t)px - (uint32_t)(ck_old >> 32);
+    const uint32_t delta = px - (uint32_t)(ck_old >> 32);
     a.chunk_px[base + j] = a.chunk_px[base + j] + (uint64_t)(int64_t)(int32_t)delta;
     for (uint32_t kk = k; kk < nvalid_old; ++kk) {
       unsigned long long& c = ck[(uint64_t)kk * a.max_chunks];
@@ -454,7 +479,7 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
   a.chunk_px[base + j] = px;
   a.last[base + j] = e | ((unsigned long long)k << 56);
   if (j + 1 < nc) {
-    const unsigned long long x = ps_pack(L.pos - D, g, dk);
+    const unsigned long long x = ps_pack(L.pos - D, dk);
     if (a.entry[base + j + 1] != x) {
       a.entry[base + j + 1] = x;
       atomicOr(changed, 1u);
@@ -469,7 +494,7 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
   __shared__ unsigned long long part[1024];
   const uint32_t f = blockIdx.x;
   if (a.status[f] != 0) return;
-  const uint32_t nc = n_chunks(a.stream_len[f], a.data_start[f]);
+  const uint32_t nc = n_chunks(a.stream_len[f], a.data_start[f], a.chunk_bits);
   const uint64_t base = (uint64_t)f * a.max_chunks;
   const uint32_t per = (nc + 1023) / 1024;
   const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, nc);
@@ -582,7 +607,7 @@ __device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t
 }
 
 struct RecGroup {
-  unsigned long long grp;   // first pixel of the aligned group, ~0: empty
+  unsigned long long grp;   // first pixel of the aligned group, ~0: empty (u64: no collision with pixels)
   uint32_t v0, v1, v2, v3, mask;
   __device__ __forceinline__ void flush(uint32_t* rec, unsigned long long lo, unsigned long long hi) {
     if (!mask) return;
@@ -614,108 +639,102 @@ struct RecGroup {
   }
 };
 
-// payload slot of grammar state g: s0 for 1,2,5,9,10; s1 for 3,6,11; s2 for 4,7,12; s3 for 8
-constexpr uint32_t SLOT0 = (1u << 1) | (1u << 2) | (1u << 5) | (1u << 9) | (1u << 10);
-constexpr uint32_t SLOT1 = (1u << 3) | (1u << 6) | (1u << 11);
-constexpr uint32_t SLOT2 = (1u << 4) | (1u << 7) | (1u << 12);
-
+// Lanes take sub-slices of DEC_EMIT_BITS: sub-slice s of slice j starts at the
+// converged parse's checkpoint (s * DEC_EMIT_BITS / 128 - 1) -- a prefix
+// position with its run digits and pixel count -- so emission parallelism does
+// not depend on the slice size the sync pass uses.
 __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
-  const uint32_t f = blockIdx.x / a.chunk_blocks;
-  const uint32_t jb = blockIdx.x % a.chunk_blocks;
+  const uint32_t f = blockIdx.x / a.emit_blocks;
+  const uint32_t vb = blockIdx.x % a.emit_blocks;
   if (a.status[f] != 0) return;
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
-  const uint32_t nc = n_chunks(len, D);
-  if (jb * 256u >= nc) return;
-  const DecTables* T = reinterpret_cast<const DecTables*>(a.tables) + f;
-  load_lut(S, T);
+  const uint32_t nc = n_chunks(len, D, a.chunk_bits);
+  const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS;
+  const uint32_t nv = nc * subs;
+  if (vb * 256u >= nv) return;
+  load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
-  if (jb * 256u + wave * 64u >= nc) return;
-  const uint32_t j = jb * 256u + threadIdx.x;
+  if (vb * 256u + wave * 64u >= nv) return;
+  const uint32_t v = vb * 256u + threadIdx.x;
+  const uint32_t j = v / subs, sub = v - j * subs;
   uint32_t* wring = ring + wave * 64u * RING_STRIDE;
   const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
   const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
   const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   const uint64_t base = (uint64_t)f * a.max_chunks;
-  const uint64_t N = (uint64_t)a.W * a.H;
-  unsigned long long q = 0, e = 0;
-  bool active = j < nc;
+  const uint32_t N = a.W * a.H;
+  const unsigned long long begin = D + (unsigned long long)j * a.chunk_bits;
+  unsigned long long q64 = 0, e = 0;
+  unsigned long long end = begin + a.chunk_bits;
+  bool active = v < nv;
   if (active) {
-    q = a.chunk_start[base + j];   // pixels accounted before this chunk
-    e = j == 0 ? 0ull : a.entry[base + j];
-    if (q > N) active = false;     // past the image: tail bytes
+    q64 = a.chunk_start[base + j];   // pixels accounted before this slice
+    const uint32_t nvalid = (uint32_t)(a.last[base + j] >> 56);
+    const unsigned long long* ck = a.ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
+    const uint32_t step = DEC_EMIT_BITS / DEC_CK_BITS;
+    if (sub == 0) {
+      e = j == 0 ? 0ull : a.entry[base + j];
+    } else {
+      const uint32_t c = sub * step - 1;
+      if (c < nvalid) {
+        const unsigned long long x = ck[(uint64_t)c * a.max_chunks];
+        e = ((begin - D) + (x & 0xFFFFu)) | ((unsigned long long)((x >> 20) & 127u) << 44);
+        q64 += x >> 32;
+      } else {
+        active = false;               // the slice's parse ended before this sub-slice
+      }
+    }
+    const uint32_t c1 = (sub + 1) * step - 1;
+    if (sub + 1 < subs && c1 < nvalid) end = begin + (ck[(uint64_t)c1 * a.max_chunks] & 0xFFFFu);
+    if (q64 > N) active = false;      // past the image: tail bytes
   }
-  const unsigned long long q0 = q;
-  const unsigned long long end = D + (unsigned long long)(j + 1) * DEC_CHUNK_BITS;
+  uint32_t q = (uint32_t)(q64 > N ? N : q64);
+  const uint32_t q0 = q;
   const unsigned long long hard = len * 8 + 64;
   uint32_t* rec = a.recs + (uint64_t)f * a.rec_stride;
   const bool strict = (a.flags & NICE_DEC_STRICT_REFERENCE) != 0;
   Lane L;
-  lane_seek(L, D + (e & ((1ull << 40) - 1)));
-  uint32_t g = (uint32_t)(e >> 40) & 15u, dk = (uint32_t)(e >> 44) & 127u;
-  // the pixel whose payload straddles our entry belongs to the previous chunk
-  bool straddle = g != 0;
+  L.pos = D + (e & ((1ull << 40) - 1));
+  L.rp = RING_W;
+  uint32_t dk = (uint32_t)(e >> 44) & 127u;
   bool closed = (q == N);          // a run completed exactly at N earlier
-  uint32_t mode = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  unsigned long long cur = 0;
   bool err = false;
   RecGroup G{~0ull, REC_RUN, REC_RUN, REC_RUN, REC_RUN, 0u};
   for (;;) {
-    const bool run = active && L.ok;
-    if (!__any(run)) {
-      if (!__any(active)) break;
-      ring_fill(wring, p, len, al16, L);
+    // at a prefix position
+    const bool at_n = q == N && (dk == 0 || closed);   // every pixel accounted for
+    if (active && (L.pos >= end || L.pos >= hard)) active = false;
+    if (!__any(active)) break;
+    if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
+    if (!active) continue;
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    const uint32_t pfx = pixel_event(L, my, S, s0, s1, s2, s3);
+    if (at_n) {
+      // the reference still reads one more prefix (code.rs:660): a run digit
+      // there makes it copy past its buffer
+      err = err || (strict && pfx >= (uint32_t)P_RUN1);
+      active = false;
       continue;
     }
-    // decode one symbol on every lane; commit where the lane's state allows
-    const uint32_t g0 = g, dk0 = dk;
-    Lane Ln = L;
-    const uint32_t sym = ring_symbol(Ln, my, S, g0);
-    uint32_t gn = g0, dkn = dk0;
-    uint64_t px = 0;
-    gstep(sym, gn, dkn, px);
-    const bool pre = g0 == 0;
-    const bool dig = pre && sym >= (uint32_t)P_RUN1;
-    const bool atpre = !straddle && pre;
-    // every pixel accounted for: the reference still reads one more prefix
-    // (code.rs:660); a run digit there makes it copy past its buffer
-    const bool stop_n = atpre && q == N && (dk0 == 0 || closed);
-    const bool stop_end = atpre && !stop_n && L.pos >= end;   // next chunk continues here
-    const bool stop_hard = L.pos >= hard;
-    err = err || (run && stop_n && !stop_hard && strict && dig);
-    const bool commit = run && !stop_n && !stop_end && !stop_hard;
-    const bool own = commit && !straddle;      // the symbol belongs to this chunk's pixels
-    const bool newpx = own && pre && !dig;
-    const unsigned long long qn = q + ((own && dig) ? px : 0ull);
-    cur = newpx ? qn : cur;
-    mode = newpx ? sym : mode;
-    closed = (own && dig) ? (closed || qn == N) : (newpx ? false : closed);
-    const unsigned long long q2 = qn + (newpx ? 1ull : 0ull);
-    const bool over = own && q2 > N;
-    if (own && !pre) {
-      s0 = ((SLOT0 >> g0) & 1u) ? sym : s0;
-      s1 = ((SLOT1 >> g0) & 1u) ? sym : s1;
-      s2 = ((SLOT2 >> g0) & 1u) ? sym : s2;
-      s3 = g0 == 8u ? sym : s3;
-    }
-    if (own && !pre && gn == 0) {            // payload complete: the record
+    const uint32_t cur = q;
+    const uint32_t c = pixel_count(pfx, dk);
+    if (pfx < (uint32_t)P_RUN1) {
       bool bad;
-      const uint32_t r = make_record(a.W, cur, mode, s0, s1, s2, s3, bad);
-      if (bad) err = true;
-      else G.put(rec, q0, cur, r);
+      const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
+      if (bad) { err = true; active = false; continue; }
+      G.put(rec, q0, cur, r);
+      q = cur + 1;
+      closed = false;
+    } else {
+      const unsigned long long qn = (unsigned long long)q + c;
+      if (qn > N) { err = true; active = false; continue; }
+      q = (uint32_t)qn;
+      closed = closed || q == N;
     }
-    if (commit) {
-      L = Ln;
-      g = gn;
-      dk = dkn;
-      q = q2;
-      straddle = straddle && gn != 0;
-    }
-    if ((run && !commit) || over || err) active = false;
-    err = err || over;
   }
   G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
   if (err) set_status(&a.status[f], NICE_E_FORMAT);

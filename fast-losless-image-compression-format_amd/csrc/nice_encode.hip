@@ -606,18 +606,30 @@ struct TileQuad {
   uint32_t nb;         // bits of the 4 pixels
 };
 
-// Loads the thread's 4 records, builds the tile's coded mask (LDS, needs a
-// barrier before use) -- phase 1.
-__device__ __forceinline__ void quad_load(const EncArgs& a, uint32_t f, int64_t start, int count, int p0,
-                                          int lane, int wid, uint32_t* mask, TileQuad& Q) {
+// The thread's 4 records of tile t (REC_UNCODED past the frame end); issued one
+// tile ahead so the loads overlap the previous tile's work.
+__device__ __forceinline__ void quad_fetch(const EncArgs& a, uint64_t t, int p0, uint32_t (&rc)[4]) {
+  const uint32_t T = a.tiles_per_frame;
+  const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+  const int64_t N = (int64_t)a.W * a.H;
+  const int64_t start = (int64_t)tt * ENC_TILE;
+  const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
   const uint32_t* rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
   if (p0 + 3 < count) {
     const uint4 v = *reinterpret_cast<const uint4*>(rp);
-    Q.rc[0] = v.x; Q.rc[1] = v.y; Q.rc[2] = v.z; Q.rc[3] = v.w;
+    rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Q.rc[q] = (p0 + q < count) ? rp[q] : REC_UNCODED;
+    for (int q = 0; q < 4; ++q) rc[q] = (p0 + q < count) ? rp[q] : REC_UNCODED;
   }
+}
+
+// Builds the tile's coded mask from the records (LDS, needs a barrier before
+// use) -- phase 1.
+__device__ __forceinline__ void quad_mask(const uint32_t (&rc)[4], int lane, int wid, uint32_t* mask,
+                                          TileQuad& Q) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Q.rc[q] = rc[q];
   Q.nib = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) Q.nib |= ((Q.rc[q] & 7u) != REC_UNCODED ? 1u : 0u) << q;
@@ -662,17 +674,31 @@ __device__ __forceinline__ void load_tbl(uint32_t* tbl, const EncArgs& a, uint32
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
 }
 
+// Contiguous tile ranges per block (the code table is reloaded only when the
+// frame changes); records are fetched one tile ahead.
+__device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& t0, uint64_t& t1) {
+  const uint64_t total = (uint64_t)a.n_frames * a.tiles_per_frame;
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+  t0 = (uint64_t)blockIdx.x * per;
+  t1 = t0 + per < total ? t0 + per : total;
+}
+
 __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t T = a.tiles_per_frame;
-  const uint64_t total = (uint64_t)a.n_frames * T;
   const int64_t N = (int64_t)a.W * a.H;
   const int p0 = 4 * threadIdx.x;
   uint32_t cur_f = 0xFFFFFFFFu;
-  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+  uint64_t t0, t1;
+  tile_range(a, t0, t1);
+  uint32_t rn[4];
+  if (t0 < t1) quad_fetch(a, t0, p0, rn);
+  for (uint64_t t = t0; t < t1; ++t) {
+    uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
+    if (t + 1 < t1) quad_fetch(a, t + 1, p0, rn);
     const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
     const int64_t start = (int64_t)tt * ENC_TILE;
@@ -680,7 +706,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
     __syncthreads();
     if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
     TileQuad Q;
-    quad_load(a, f, start, count, p0, lane, wid, mask, Q);
+    quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
     quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
     uint32_t x = Q.nb;
@@ -740,7 +766,14 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
   const int p0 = 4 * threadIdx.x;
   uint32_t cur_f = 0xFFFFFFFFu;
   uint32_t used_words = PACK_MAX_WORDS;
-  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+  uint64_t t0, t1;
+  tile_range(a, t0, t1);
+  (void)total;
+  uint32_t rn[4];
+  if (t0 < t1) quad_fetch(a, t0, p0, rn);
+  for (uint64_t t = t0; t < t1; ++t) {
+    uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
+    if (t + 1 < t1) quad_fetch(a, t + 1, p0, rn);
     const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // enc_serial's frame
     const int64_t start = (int64_t)tt * ENC_TILE;
@@ -749,7 +782,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
     for (uint32_t w = threadIdx.x; w < used_words; w += ENC_THREADS) bits[w] = 0;
     if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
     TileQuad Q;
-    quad_load(a, f, start, count, p0, lane, wid, mask, Q);
+    quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
     quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
     uint32_t x = Q.nb;

@@ -56,9 +56,10 @@ __global__ void enc_serial(EncArgs a);
 
 namespace nice {
 
-constexpr uint32_t DEC_CHUNK_BITS = 2048;   // speculative-parse slice
 constexpr uint32_t DEC_CK_BITS = 128;       // sync checkpoint spacing inside a chunk
-constexpr uint32_t DEC_N_CK = DEC_CHUNK_BITS / DEC_CK_BITS - 1;
+constexpr uint32_t DEC_MIN_CHUNK_BITS = 1024;   // speculative-parse slice: a power of two
+constexpr uint32_t DEC_MAX_CHUNK_BITS = 16384;  // chosen per call (nice_capi.hip)
+constexpr uint32_t DEC_EMIT_BITS = 1024;        // record-emission sub-slice (<= the slice)
 constexpr int DEC_MAX_SEGS = 64;            // one lane per row segment
 
 struct DecArgs {
@@ -76,7 +77,9 @@ struct DecArgs {
   uint32_t max_chunks, chunk_blocks;  // per frame
   unsigned long long* entry;          // n_frames * max_chunks packed entry states
   unsigned long long* last;           // n_frames * max_chunks entry of the last parse
-  unsigned long long* ck;             // n_frames * DEC_N_CK * max_chunks checkpoints
+  unsigned long long* ck;             // n_frames * n_ck * max_chunks checkpoints
+  uint32_t chunk_bits, n_ck;          // slice size; checkpoints per slice (chunk_bits / 128 - 1)
+  uint32_t emit_blocks;               // per frame: ceil(max_chunks * chunk_bits / DEC_EMIT_BITS / 256)
   unsigned long long* chunk_px;       // n_frames * max_chunks
   unsigned long long* chunk_start;    // n_frames * max_chunks
   uint32_t* recs;                     // n_frames * rec_stride per-pixel records

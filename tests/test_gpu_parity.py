@@ -134,3 +134,29 @@ def test_batch_device_roundtrip(nice, O):
     assert (status.cpu().numpy() == 0).all()
     got = dec.cpu().numpy().reshape(n, -1, 4)
     assert np.array_equal(got[:, :, :3], frames.reshape(n, -1, 4)[:, :, :3])
+
+
+@pytest.mark.parametrize("bits", [2048, 16384])
+def test_decode_long_slices(nice, O, bits, monkeypatch):
+    """Long parse slices: emission runs from checkpoint sub-slices (the default
+    picks them only for large batches)."""
+    monkeypatch.setenv("NICE_DEC_SLICE_BITS", str(bits))
+    for name, px, w, h, c in CASES:
+        if name not in ("syn512x4", "syn1920x1080x4", "stripes700x300x3", "noise300x200x3"):
+            continue
+        s = O.encode(px, w, h, c)
+        got, _ = nice.decode_bytes(s)
+        g = np.frombuffer(got, np.uint8).reshape(-1, c)
+        assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), name
+
+
+def test_decode_single_wave_rows(nice, O, monkeypatch):
+    """The single-wave row kernel (used for W < 64 or W > 16384) on wide images."""
+    monkeypatch.setenv("NICE_DEC_SINGLE_WAVE", "1")
+    for name, px, w, h, c in CASES:
+        if name not in ("syn512x4", "odd37x23x4", "palette333x90x3"):
+            continue
+        s = O.encode(px, w, h, c)
+        got, _ = nice.decode_bytes(s)
+        g = np.frombuffer(got, np.uint8).reshape(-1, c)
+        assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), name
