@@ -604,6 +604,7 @@ struct TileQuad {
   uint32_t nib;        // coded flags of the 4 pixels
   uint64_t run[4];     // run after each coded pixel
   uint32_t nb;         // bits of the 4 pixels
+  uint32_t e[4][5];    // code table entries: prefix + up to 4 payload symbols (0: none)
 };
 
 // The thread's 4 records of tile t (REC_UNCODED past the frame end); issued one
@@ -640,7 +641,8 @@ __device__ __forceinline__ void quad_mask(const uint32_t (&rc)[4], int lane, int
   if ((lane & 7) == 0) mask[wid * 8 + (lane >> 3)] = mw;
 }
 
-// Runs and bit counts -- phase 2 (after the mask barrier).
+// Runs, code entries and bit counts -- phase 2 (after the mask barrier).
+// Branch-free apart from the run digits: absent symbols get entry 0 (length 0).
 __device__ __forceinline__ void quad_bits(const uint32_t* tbl, const uint32_t* mask, int64_t start, int count,
                                           int p0, uint32_t next_tile_px, TileQuad& Q) {
   const int nx_local = next_coded_local(mask, p0 + 3);
@@ -648,23 +650,26 @@ __device__ __forceinline__ void quad_bits(const uint32_t* tbl, const uint32_t* m
   Q.nb = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    Q.run[q] = 0;
-    if ((Q.nib >> q) & 1u) {
-      const uint32_t later = Q.nib >> (q + 1);
-      const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
-      Q.run[q] = nxt - (uint64_t)(start + p0 + q) - 1;
-      uint32_t b0, b1, b2, b3;
-      const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
-      Q.nb += (tbl[BIN_PREFIX + (Q.rc[q] & 7u)] & 31u) + (tbl[b0] & 31u);
-      if (n > 1) Q.nb += (tbl[b1] & 31u) + (tbl[b2] & 31u);
-      if (n > 3) Q.nb += tbl[b3] & 31u;
-      if (Q.run[q] > 0) {
-        uint64_t m = Q.run[q] - 1;
-        while (true) {
-          Q.nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
-          if (m < 8) break;
-          m >>= 3;
-        }
+    const bool coded = (Q.nib >> q) & 1u;
+    uint32_t b0, b1, b2, b3;
+    const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
+    const uint32_t t0 = tbl[BIN_PREFIX + min(Q.rc[q] & 7u, 4u)], t1 = tbl[b0], t2 = tbl[b1], t3 = tbl[b2],
+                   t4 = tbl[b3];
+    Q.e[q][0] = coded ? t0 : 0u;
+    Q.e[q][1] = coded ? t1 : 0u;
+    Q.e[q][2] = (coded && n > 1) ? t2 : 0u;
+    Q.e[q][3] = (coded && n > 1) ? t3 : 0u;
+    Q.e[q][4] = (coded && n > 3) ? t4 : 0u;
+    Q.nb += (Q.e[q][0] & 31u) + (Q.e[q][1] & 31u) + (Q.e[q][2] & 31u) + (Q.e[q][3] & 31u) + (Q.e[q][4] & 31u);
+    const uint32_t later = Q.nib >> (q + 1);
+    const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
+    Q.run[q] = coded ? nxt - (uint64_t)(start + p0 + q) - 1 : 0u;
+    if (Q.run[q] > 0) {
+      uint64_t m = Q.run[q] - 1;
+      while (true) {
+        Q.nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
+        if (m < 8) break;
+        m >>= 3;
       }
     }
   }
@@ -804,8 +809,8 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
       uint64_t acc = 0;
       uint32_t nacc = pos & 31u, wi = pos >> 5;
       auto put = [&](uint32_t e) {
-        const uint32_t n = e & 31u;
-        acc |= (uint64_t)(e >> 5) << (64u - nacc - n);
+        const uint32_t n = e & 31u;   // 0: no symbol (e == 0)
+        acc |= (uint64_t)(e >> 5) << ((64u - nacc - n) & 63u);
         nacc += n;
         if (nacc >= 32u) {
           atomicOr(&bits[wi], (uint32_t)(acc >> 32));
@@ -816,20 +821,17 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
       };
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if ((Q.nib >> q) & 1u) {
-          uint32_t b0, b1, b2, b3;
-          const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
-          put(tbl[BIN_PREFIX + (Q.rc[q] & 7u)]);
-          put(tbl[b0]);
-          if (n > 1) { put(tbl[b1]); put(tbl[b2]); }
-          if (n > 3) put(tbl[b3]);
-          if (Q.run[q] > 0) {
-            uint64_t m = Q.run[q] - 1;
-            while (true) {
-              put(tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)]);
-              if (m < 8) break;
-              m >>= 3;
-            }
+        put(Q.e[q][0]);
+        put(Q.e[q][1]);
+        put(Q.e[q][2]);
+        put(Q.e[q][3]);
+        put(Q.e[q][4]);
+        if (Q.run[q] > 0) {
+          uint64_t m = Q.run[q] - 1;
+          while (true) {
+            put(tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)]);
+            if (m < 8) break;
+            m >>= 3;
           }
         }
       }
