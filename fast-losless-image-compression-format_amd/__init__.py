@@ -44,6 +44,8 @@ EXPORTS = [
     "nice_version", "nice_device_count", "nice_encode_bound", "nice_encode", "nice_peek_header",
     "nice_decode", "nice_ctx_create", "nice_ctx_destroy", "nice_ctx_reserve",
     "nice_encode_batch_dev", "nice_decode_batch_dev",
+    "nice_band_classify", "nice_band_runs", "nice_band_tables", "nice_band_words", "nice_band_pack",
+    "nice_band_assemble", "nice_tile_pixels",
 ]
 
 

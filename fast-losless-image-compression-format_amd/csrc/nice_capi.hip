@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/nice.h"
@@ -130,11 +131,18 @@ struct PhaseTimer {
   }
 };
 
+struct BandState {
+  bool classified = false, tabled = false;
+  nice::EncArgs a{};
+  uint64_t band_bits = 0, seed_bit = 0;
+};
+
 struct nice_ctx {
   int device = 0;
   std::mutex mu;
-  Arena enc, dec, host_px, host_out, dev_len;
+  Arena enc, dec, host_px, host_out, dev_len, band, band_hdr;
   PhaseTimer timer;
+  BandState bs;
 };
 
 extern "C" {
@@ -199,6 +207,48 @@ int nice_ctx_reserve(nice_ctx* ctx, uint32_t n_frames, uint32_t w, uint32_t h) {
   return ctx->enc.grow(L.total);
 }
 
+}  // extern "C"
+
+namespace {
+EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t w, uint32_t h,
+                 uint8_t channels, uint8_t channels_out, uint32_t T, uint64_t N) {
+  EncArgs a{};
+  a.n_frames = n_frames;
+  a.W = w;
+  a.H = h;
+  a.C = channels;
+  a.channels_out = channels_out;
+  a.tiles_per_frame = T;
+  a.hist = (uint32_t*)(base + L.o_hist);
+  a.frame_flags = (uint32_t*)(base + L.o_flags);
+  a.tile_first = (uint32_t*)(base + L.o_first);
+  a.tile_last = (uint32_t*)(base + L.o_last);
+  a.tile_next = (uint32_t*)(base + L.o_next);
+  a.tbl = (uint32_t*)(base + L.o_tbl);
+  a.tbl_code = (uint32_t*)(base + L.o_tblcode);
+  a.tbl_len8 = base + L.o_len8;
+  a.stream_max = base + L.o_smax;
+  a.seed_bit = (unsigned long long*)(base + L.o_seedbit);
+  a.seed_suf = (uint32_t*)(base + L.o_seedsuf);
+  a.hdr_bytes = (unsigned long long*)(base + L.o_hdrbytes);
+  a.hdr_cache = (uint32_t*)(base + L.o_hdrcache);
+  a.hdr_bitoff = base + L.o_hdrbitoff;
+  a.recs = (uint32_t*)(base + L.o_recs);
+  a.rec_stride = (N + 3) & ~3ull;
+  a.tile_bits = (uint32_t*)(base + L.o_tbits);
+  a.tile_off = (unsigned long long*)(base + L.o_toff);
+  a.data_end = (unsigned long long*)(base + L.o_dend);
+  a.tile_lo = 0;
+  a.tile_hi = T;
+  a.px_lo = 0;
+  a.px_hi = (int64_t)N;
+  a.band = 0;
+  return a;
+}
+}  // namespace
+
+extern "C" {
+
 int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t frame_stride,
                           uint32_t n_frames, uint32_t w, uint32_t h, uint8_t channels,
                           uint8_t channels_out, uint8_t* d_out, uint64_t out_stride,
@@ -220,38 +270,12 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   int rc = ctx->enc.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->enc.ptr;
-  EncArgs a{};
+  EncArgs a = enc_args(L, base, n_frames, w, h, channels, channels_out, T, N);
   a.px = d_px;
   a.frame_stride = frame_stride;
-  a.n_frames = n_frames;
-  a.W = w;
-  a.H = h;
-  a.C = channels;
-  a.channels_out = channels_out;
-  a.tiles_per_frame = T;
   a.out = d_out;
   a.out_stride = out_stride;
   a.out_len = (unsigned long long*)d_out_len;
-  a.hist = (uint32_t*)(base + L.o_hist);
-  a.frame_flags = (uint32_t*)(base + L.o_flags);
-  a.tile_first = (uint32_t*)(base + L.o_first);
-  a.tile_last = (uint32_t*)(base + L.o_last);
-  a.tile_next = (uint32_t*)(base + L.o_next);
-  a.tbl = (uint32_t*)(base + L.o_tbl);
-  a.tbl_code = (uint32_t*)(base + L.o_tblcode);
-  a.tbl_len8 = base + L.o_len8;
-  a.stream_max = base + L.o_smax;
-  a.seed_bit = (unsigned long long*)(base + L.o_seedbit);
-  a.seed_suf = (uint32_t*)(base + L.o_seedsuf);
-  a.hdr_bytes = (unsigned long long*)(base + L.o_hdrbytes);
-  a.hdr_cache = (uint32_t*)(base + L.o_hdrcache);
-  a.hdr_bitoff = base + L.o_hdrbitoff;
-  a.recs = (uint32_t*)(base + L.o_recs);
-  a.rec_stride = (N + 3) & ~3ull;
-  a.tile_bits = (uint32_t*)(base + L.o_tbits);
-  a.tile_off = (unsigned long long*)(base + L.o_toff);
-  a.data_end = (unsigned long long*)(base + L.o_dend);
-
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
   const uint64_t total_tiles = (uint64_t)n_frames * T;
   if (T > 0) {
@@ -548,6 +572,167 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
             h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
     (void)hipFree(dstats);
   }
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+// ---- one image sharded over ranks ------------------------
+int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t px0, uint64_t px_count,
+                       uint32_t w, uint32_t h, uint8_t channels, uint8_t channels_out, uint32_t tile_lo,
+                       uint32_t tile_hi, uint32_t* d_edges) {
+  if (!ctx || !d_px || !d_edges || (channels != 3 && channels != 4)) return NICE_E_ARG;
+  const uint64_t N = (uint64_t)w * h;
+  const uint32_t T = tiles_for(w, h);
+  if (N == 0 || N > (1ull << 30) || tile_lo >= tile_hi || tile_hi > T) return NICE_E_ARG;
+  // pixel memory must hold the band and the 3 rows + 3 pixels its references reach
+  const uint64_t band_px0 = (uint64_t)tile_lo * ENC_TILE;
+  const uint64_t band_px1 = std::min<uint64_t>((uint64_t)tile_hi * ENC_TILE, N);
+  const uint64_t need0 = band_px0 > 3ull * w + 3 ? band_px0 - 3ull * w - 3 : 0;
+  if (px0 > need0 || px0 + px_count < band_px1 || px0 + px_count > N) return NICE_E_ARG;
+  if (channels == 4 && ((uintptr_t)d_px & 3)) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  EncLayout L = enc_layout(1, T, band_px1 - band_px0);
+  int rc = ctx->band.grow(L.total);
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)ctx->band.ptr;
+  EncArgs a = enc_args(L, base, 1, w, h, channels, channels_out, T, N);
+  // virtual bases: global pixel index g addresses d_px + (g - px0) * channels,
+  // band records are stored from the band's first pixel
+  a.px = d_px - (int64_t)px0 * channels;
+  a.frame_stride = 0;
+  a.recs = (uint32_t*)(base + L.o_recs) - band_px0;
+  a.tile_lo = tile_lo;
+  a.tile_hi = tile_hi;
+  a.px_lo = (int64_t)px0;
+  a.px_hi = (int64_t)(px0 + px_count);
+  a.band = 1;
+  NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
+  const uint64_t work = tile_hi - tile_lo;
+  uint64_t blocks = 2048, per = (work + blocks - 1) / blocks;
+  if (per < 1) per = 1;
+  blocks = (work + per - 1) / per;
+  a.tiles_per_block = (uint32_t)per;
+  hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_band_edges, dim3(1), dim3(256), 0, st, a, d_edges);
+  NICE_HIP(hipGetLastError());
+  ctx->bs = BandState{};
+  ctx->bs.a = a;
+  ctx->bs.classified = true;
+  return NICE_OK;
+}
+
+int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_hist) {
+  if (!ctx || !d_hist || !ctx->bs.classified) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  EncArgs& a = ctx->bs.a;
+  a.band_next = band_next;
+  hipLaunchKernelGGL(enc_tailruns, dim3(1), dim3(1024), 0, st, a);
+  NICE_HIP(hipMemcpyAsync(d_hist, a.hist, N_BINS * 4, hipMemcpyDeviceToDevice, st));
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, uint64_t* band_bits,
+                     uint64_t* seed_bit) {
+  if (!ctx || !d_hist_total || !ctx->bs.classified) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  EncArgs& a = ctx->bs.a;
+  int rc = ctx->band_hdr.grow(4096 + 16);
+  if (rc) return rc;
+  NICE_HIP(hipMemcpyAsync(a.hist, d_hist_total, N_BINS * 4, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(enc_tables, dim3(N_STREAMS), dim3(64), 0, st, a);
+  EncArgs h = a;   // the header goes to the context's header buffer
+  h.out = (uint8_t*)ctx->band_hdr.ptr;
+  h.out_stride = 4096;
+  h.out_len = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
+  hipLaunchKernelGGL(enc_header, dim3(1), dim3(64), 0, st, h);
+  hipLaunchKernelGGL(enc_tilebits, dim3(std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u)), dim3(256), 0, st, a);
+  unsigned long long* info = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
+  hipLaunchKernelGGL(enc_band_sum, dim3(1), dim3(256), 0, st, a, info);
+  unsigned long long hinfo[2];
+  uint32_t flags = 0;
+  NICE_HIP(hipMemcpyAsync(hinfo, info, 16, hipMemcpyDeviceToHost, st));
+  NICE_HIP(hipMemcpyAsync(&flags, a.frame_flags, 4, hipMemcpyDeviceToHost, st));
+  NICE_HIP(hipStreamSynchronize(st));
+  // codes longer than 25 bits need the serial writer over the whole image
+  if (flags & FLAG_SERIAL) return NICE_E_UNSUPPORTED;
+  ctx->bs.band_bits = hinfo[0];
+  ctx->bs.seed_bit = hinfo[1];
+  ctx->bs.tabled = true;
+  if (band_bits) *band_bits = hinfo[0];
+  if (seed_bit) *seed_bit = hinfo[1];
+  return NICE_OK;
+}
+
+uint32_t nice_tile_pixels(void) { return ENC_TILE; }
+
+uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits) {
+  return band_bits ? ((band_bit0 + band_bits + 31) >> 5) - (band_bit0 >> 5) : 0;
+}
+
+int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_words, uint64_t words_cap) {
+  if (!ctx || !ctx->bs.tabled) return NICE_E_ARG;
+  const uint64_t nw = nice_band_words(band_bit0, ctx->bs.band_bits);
+  if (nw > words_cap || (nw && !d_words) || band_bit0 < ctx->bs.seed_bit) return NICE_E_ARG;
+  if (nw == 0) return NICE_OK;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  EncArgs a = ctx->bs.a;
+  a.band_bit0 = band_bit0;
+  a.out = (uint8_t*)d_words - (int64_t)(band_bit0 >> 5) * 4;   // virtual: stream word w at d_words[w - w0]
+  a.out_stride = 0;
+  hipLaunchKernelGGL(enc_tilescan, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(enc_pack, dim3(std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u)), dim3(256), 0, st, a);
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, const uint64_t* band_bit0,
+                       const uint64_t* band_bits, uint32_t n_bands, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* out_len) {
+  if (!ctx || !ctx->bs.tabled || !d_out || !out_len || n_bands == 0 || !band_bit0 || !band_bits)
+    return NICE_E_ARG;
+  const uint64_t seed = ctx->bs.seed_bit;
+  std::vector<unsigned long long> meta(2 * n_bands + 1);
+  uint64_t off = 0, end = seed;
+  for (uint32_t r = 0; r < n_bands; ++r) {
+    if (band_bit0[r] != end) return NICE_E_ARG;   // bands must tile the data bits
+    meta[r] = band_bit0[r] >> 5;
+    meta[n_bands + r] = off;
+    off += nice_band_words(band_bit0[r], band_bits[r]);
+    end += band_bits[r];
+  }
+  meta[2 * n_bands] = off;
+  const uint64_t B = end >> 3;
+  if (B + 5 > out_cap || (((uintptr_t)d_out) & 3)) return NICE_E_CAPACITY;
+  NICE_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  int rc = ctx->dev_len.grow(meta.size() * 8 + 64);
+  if (rc) return rc;
+  unsigned long long* dmeta = (unsigned long long*)ctx->dev_len.ptr;
+  NICE_HIP(hipMemcpyAsync(dmeta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, st));
+  // header words (the last one zero padded), then the bands, then the tail
+  NICE_HIP(hipMemcpyAsync(d_out, ctx->band_hdr.ptr, ((seed + 31) >> 5) * 4, hipMemcpyDeviceToDevice, st));
+  // words past the header up to the end are written by the bands (first/last OR-ed)
+  const uint64_t hdr_words = (seed + 31) >> 5, end_words = (end + 31) >> 5;
+  if (end_words > hdr_words)
+    NICE_HIP(hipMemsetAsync(d_out + hdr_words * 4, 0, (end_words - hdr_words) * 4, st));
+  if (off)
+    hipLaunchKernelGGL(enc_band_merge, dim3(64, n_bands), dim3(256), 0, st, (uint32_t*)d_out, d_words, dmeta,
+                       dmeta + n_bands, n_bands);
+  EncArgs a = ctx->bs.a;
+  a.out = d_out;
+  a.out_stride = 0;
+  a.n_frames = 1;
+  a.data_end = dmeta + 2 * n_bands + 1;
+  a.out_len = dmeta + 2 * n_bands + 2;
+  NICE_HIP(hipMemcpyAsync(a.data_end, &end, 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(enc_tail, dim3(1), dim3(64), 0, st, a);
+  NICE_HIP(hipStreamSynchronize(st));   // `end` lives on this stack frame
+  *out_len = B + 5;
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }

@@ -53,12 +53,12 @@ __device__ __forceinline__ uint32_t load_spread(const uint8_t* __restrict__ fram
 }
 
 __device__ inline void stage_tile(TileWin& tw, const uint8_t* __restrict__ frame, int64_t start,
-                                  int64_t N, uint32_t W, int C) {
+                                  int64_t lo, int64_t hi, uint32_t W, int C) {
   for (int k = 0; k < 4; ++k) {
     const int64_t base = start - (int64_t)k * W - 3;
     for (int j = threadIdx.x; j < WIN; j += ENC_THREADS) {
       const int64_t g = base + j;
-      tw.w[k][j] = (g >= 0 && g < N) ? load_spread(frame, g, C) : 0u;
+      tw.w[k][j] = (g >= lo && g < hi) ? load_spread(frame, g, C) : 0u;
     }
   }
 }
@@ -71,7 +71,7 @@ struct TilePrefetch {
   uint32_t v[4][STAGE_PER_THREAD];
 };
 __device__ __forceinline__ void prefetch_tile(TilePrefetch& pf, const uint8_t* __restrict__ frame,
-                                              int64_t start, int64_t N, uint32_t W) {
+                                              int64_t start, int64_t lo, int64_t hi, uint32_t W) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t base = start - (int64_t)k * W - 3;
@@ -79,7 +79,7 @@ __device__ __forceinline__ void prefetch_tile(TilePrefetch& pf, const uint8_t* _
     for (int i = 0; i < STAGE_PER_THREAD; ++i) {
       const int j = (int)threadIdx.x + i * ENC_THREADS;
       const int64_t g = base + j;
-      pf.v[k][i] = (j < WIN && g >= 0 && g < N) ? reinterpret_cast<const uint32_t*>(frame)[g] : 0u;
+      pf.v[k][i] = (j < WIN && g >= lo && g < hi) ? reinterpret_cast<const uint32_t*>(frame)[g] : 0u;
     }
   }
 }
@@ -207,27 +207,30 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
   __shared__ uint32_t hist[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
 
-  const uint64_t total_tiles = (uint64_t)a.n_frames * a.tiles_per_frame;
-  const uint64_t t_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
-  uint64_t t_end = t_begin + a.tiles_per_block;
-  if (t_end > total_tiles) t_end = total_tiles;
-  if (t_begin >= t_end) return;
+  // work items: frame f, band tile tt in [tile_lo, tile_hi); t = f*T + tt
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint64_t total_work = (uint64_t)a.n_frames * nt;
+  const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
+  uint64_t w_end = w_begin + a.tiles_per_block;
+  if (w_end > total_work) w_end = total_work;
+  if (w_begin >= w_end) return;
 
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) hist[b] = 0;
-  uint32_t cur_frame = (uint32_t)(t_begin / a.tiles_per_frame);
+  uint32_t cur_frame = (uint32_t)(w_begin / nt);
   const int lane = threadIdx.x & 63;
   const int64_t N = (int64_t)a.W * a.H;
   const bool rgba = a.C == 4;
   TilePrefetch pf;
   if (rgba) {
-    const uint32_t f0 = (uint32_t)(t_begin / a.tiles_per_frame);
+    const uint32_t f0 = (uint32_t)(w_begin / nt);
     prefetch_tile(pf, a.px + (uint64_t)f0 * a.frame_stride,
-                  (int64_t)(t_begin % a.tiles_per_frame) * ENC_TILE, N, a.W);
+                  (int64_t)(a.tile_lo + w_begin % nt) * ENC_TILE, a.px_lo, a.px_hi, a.W);
   }
 
-  for (uint64_t t = t_begin; t < t_end; ++t) {
-    const uint32_t f = (uint32_t)(t / a.tiles_per_frame);
-    const uint32_t tt = (uint32_t)(t % a.tiles_per_frame);
+  for (uint64_t w = w_begin; w < w_end; ++w) {
+    const uint32_t f = (uint32_t)(w / nt);
+    const uint32_t tt = a.tile_lo + (uint32_t)(w % nt);
+    const uint64_t t = (uint64_t)f * a.tiles_per_frame + tt;
     if (f != cur_frame) {
       __syncthreads();
       for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) {
@@ -242,13 +245,13 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
     __syncthreads();
     if (rgba) {
       commit_tile(tw, pf);
-      if (t + 1 < t_end) {   // next tile's pixels are in flight while this one is classified
-        const uint32_t f1 = (uint32_t)((t + 1) / a.tiles_per_frame);
+      if (w + 1 < w_end) {   // next tile's pixels are in flight while this one is classified
+        const uint32_t f1 = (uint32_t)((w + 1) / nt);
         prefetch_tile(pf, a.px + (uint64_t)f1 * a.frame_stride,
-                      (int64_t)((t + 1) % a.tiles_per_frame) * ENC_TILE, N, a.W);
+                      (int64_t)(a.tile_lo + (w + 1) % nt) * ENC_TILE, a.px_lo, a.px_hi, a.W);
       }
     } else {
-      stage_tile(tw, frame, start, N, a.W, a.C);
+      stage_tile(tw, frame, start, a.px_lo, a.px_hi, a.W, a.C);
     }
     __syncthreads();
 
@@ -336,11 +339,14 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
   __shared__ uint32_t chunk_min[TR_THREADS];
   const uint32_t f = blockIdx.x;
   const uint32_t T = a.tiles_per_frame;
-  const uint64_t base = (uint64_t)f * T;
+  const uint64_t base = (uint64_t)f * T + a.tile_lo;
+  const uint32_t nt = a.tile_hi - a.tile_lo;
   const uint32_t N = a.W * a.H;
-  const uint32_t per = (T + TR_THREADS - 1) / TR_THREADS;
+  // the first coded pixel after the band (frames: none)
+  const uint32_t after = a.band ? (uint32_t)a.band_next : NONE;
+  const uint32_t per = (nt + TR_THREADS - 1) / TR_THREADS;
   const uint32_t c0 = threadIdx.x * per;
-  const uint32_t c1 = min(c0 + per, T);
+  const uint32_t c1 = min(c0 + per, nt);
   uint32_t m = NONE;
   for (uint32_t t = c0; t < c1; ++t) m = min(m, a.tile_first[base + t]);
   chunk_min[threadIdx.x] = m;
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
     chunk_min[threadIdx.x] = v;
     __syncthreads();
   }
-  uint32_t nxt = (threadIdx.x + 1 < TR_THREADS) ? chunk_min[threadIdx.x + 1] : NONE;
+  uint32_t nxt = min((threadIdx.x + 1 < TR_THREADS) ? chunk_min[threadIdx.x + 1] : NONE, after);
   for (int64_t t = (int64_t)c1 - 1; t >= (int64_t)c0; --t) {
     const uint32_t next_px = (nxt == NONE) ? N : nxt;
     a.tile_next[base + t] = next_px;
@@ -681,11 +687,16 @@ __device__ __forceinline__ void load_tbl(uint32_t* tbl, const EncArgs& a, uint32
 
 // Contiguous tile ranges per block (the code table is reloaded only when the
 // frame changes); records are fetched one tile ahead.
-__device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& t0, uint64_t& t1) {
-  const uint64_t total = (uint64_t)a.n_frames * a.tiles_per_frame;
+// Work items w in [w0, w1): frame w / nt, band tile tile_lo + w % nt.
+__device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& w0, uint64_t& w1) {
+  const uint64_t total = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
   const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
-  t0 = (uint64_t)blockIdx.x * per;
-  t1 = t0 + per < total ? t0 + per : total;
+  w0 = (uint64_t)blockIdx.x * per;
+  w1 = w0 + per < total ? w0 + per : total;
+}
+__device__ __forceinline__ uint64_t work_tile(const EncArgs& a, uint64_t w) {
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  return (w / nt) * a.tiles_per_frame + a.tile_lo + (uint32_t)(w % nt);
 }
 
 __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
@@ -700,10 +711,11 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   uint64_t t0, t1;
   tile_range(a, t0, t1);
   uint32_t rn[4];
-  if (t0 < t1) quad_fetch(a, t0, p0, rn);
-  for (uint64_t t = t0; t < t1; ++t) {
+  if (t0 < t1) quad_fetch(a, work_tile(a, t0), p0, rn);
+  for (uint64_t w = t0; w < t1; ++w) {
+    const uint64_t t = work_tile(a, w);
     uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    if (t + 1 < t1) quad_fetch(a, t + 1, p0, rn);
+    if (w + 1 < t1) quad_fetch(a, work_tile(a, w + 1), p0, rn);
     const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
     const int64_t start = (int64_t)tt * ENC_TILE;
@@ -728,10 +740,10 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   __shared__ unsigned long long part[1024];
   const uint32_t f = blockIdx.x;
   if (a.frame_flags[f] & FLAG_SERIAL) return;
-  const uint32_t T = a.tiles_per_frame;
-  const uint64_t base = (uint64_t)f * T;
-  const uint32_t per = (T + 1023) / 1024;
-  const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, T);
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo;
+  const uint32_t per = (nt + 1023) / 1024;
+  const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, nt);
   unsigned long long sum = 0;
   for (uint32_t t = c0; t < c1; ++t) sum += a.tile_bits[base + t];
   part[threadIdx.x] = sum;
@@ -742,20 +754,22 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
     part[threadIdx.x] += v;
     __syncthreads();
   }
-  const uint64_t seed = a.seed_bit[f];
-  const uint64_t seed_word = seed >> 5;
+  // frames: data starts after the header, whose last word is already zero
+  // padded; bands: at band_bit0, and every partial word is shared (zeroed)
+  const uint64_t seed = a.band ? a.band_bit0 : a.seed_bit[f];
+  const int64_t seed_word = a.band ? (int64_t)(seed >> 5) - 1 : (int64_t)(seed >> 5);
   uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
   unsigned long long run = seed + (threadIdx.x ? part[threadIdx.x - 1] : 0ull);
   for (uint32_t t = c0; t < c1; ++t) {
     a.tile_off[base + t] = run;
     // a word shared with the previous tile (or the header: pre-padded with zeros)
-    if ((run & 31) && (run >> 5) > seed_word) out32[run >> 5] = 0u;
+    if ((run & 31) && (int64_t)(run >> 5) > seed_word) out32[run >> 5] = 0u;
     run += a.tile_bits[base + t];
   }
   if (threadIdx.x == 1023) {
     const uint64_t end = seed + part[1023];
     a.data_end[f] = end;
-    if ((end & 31) && (end >> 5) > seed_word) out32[end >> 5] = 0u;
+    if ((end & 31) && (int64_t)(end >> 5) > seed_word) out32[end >> 5] = 0u;
   }
 }
 
@@ -775,10 +789,11 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
   tile_range(a, t0, t1);
   (void)total;
   uint32_t rn[4];
-  if (t0 < t1) quad_fetch(a, t0, p0, rn);
-  for (uint64_t t = t0; t < t1; ++t) {
+  if (t0 < t1) quad_fetch(a, work_tile(a, t0), p0, rn);
+  for (uint64_t w = t0; w < t1; ++w) {
+    const uint64_t t = work_tile(a, w);
     uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    if (t + 1 < t1) quad_fetch(a, t + 1, p0, rn);
+    if (w + 1 < t1) quad_fetch(a, work_tile(a, w + 1), p0, rn);
     const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // enc_serial's frame
     const int64_t start = (int64_t)tt * ENC_TILE;
@@ -929,6 +944,70 @@ __global__ __launch_bounds__(64) void enc_serial(EncArgs a) {
   out[bw.pos + 3] = (uint8_t)(bw.cache >> 8);
   out[bw.pos + 4] = (uint8_t)(bw.cache);
   a.out_len[f] = bw.pos + 5;
+}
+
+}  // namespace nice
+
+namespace nice {
+
+// ---------------------------------------------------------------------------
+// Band assembly (one image sharded over ranks): OR the bands' word arrays into
+// the stream (header words are already there, zero padded), then the tail.
+// band_w0[r]: first stream word of band r; band_off[r]: its first word in the
+// concatenated array; band_off[R]: total words.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_band_merge(uint32_t* out32, const uint32_t* words,
+                                                      const unsigned long long* band_w0,
+                                                      const unsigned long long* band_off, uint32_t R) {
+  const uint32_t r = blockIdx.y;
+  if (r >= R) return;
+  const unsigned long long n = band_off[r + 1] - band_off[r];
+  const unsigned long long w0 = band_w0[r];
+  for (unsigned long long m = (unsigned long long)blockIdx.x * 256 + threadIdx.x; m < n;
+       m += (unsigned long long)gridDim.x * 256) {
+    const uint32_t v = words[band_off[r] + m];
+    if (m == 0 || m + 1 == n) atomicOr(&out32[w0 + m], v);   // shared with a neighbour or the header
+    else out32[w0 + m] = v;
+  }
+}
+
+}  // namespace nice
+
+namespace nice {
+
+// Band helpers: first/last coded pixel of the band (over tiles [tile_lo,
+// tile_hi) of frame 0), and the band's total data bits.
+__global__ __launch_bounds__(256) void enc_band_edges(EncArgs a, uint32_t* edges) {
+  __shared__ uint32_t s_first, s_last;
+  if (threadIdx.x == 0) { s_first = NONE; s_last = 0; }
+  __syncthreads();
+  uint32_t fi = NONE, la = 0;
+  bool any = false;
+  for (uint32_t t = a.tile_lo + threadIdx.x; t < a.tile_hi; t += 256) {
+    fi = min(fi, a.tile_first[t]);
+    if (a.tile_last[t] != NONE) { la = max(la, a.tile_last[t]); any = true; }
+  }
+  atomicMin(&s_first, fi);
+  if (any) atomicMax(&s_last, la);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    edges[0] = s_first;
+    edges[1] = s_first == NONE ? NONE : s_last;
+  }
+}
+
+__global__ __launch_bounds__(256) void enc_band_sum(EncArgs a, unsigned long long* info) {
+  __shared__ unsigned long long s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  unsigned long long v = 0;
+  for (uint32_t t = a.tile_lo + threadIdx.x; t < a.tile_hi; t += 256) v += a.tile_bits[t];
+  atomicAdd(&s, v);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    info[0] = s;
+    info[1] = a.seed_bit[0];
+  }
 }
 
 }  // namespace nice

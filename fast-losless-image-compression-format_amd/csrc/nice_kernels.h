@@ -40,6 +40,16 @@ struct EncArgs {
   uint32_t* tile_bits;       // n_frames * T: data bits per tile
   unsigned long long* tile_off;   // n_frames * T: absolute bit offset of each tile
   unsigned long long* data_end;   // n_frames: bit position after the last data bit
+  // Band mode (one image sharded over ranks): only tiles
+  // [tile_lo, tile_hi) of each frame are processed; pixel memory is valid for
+  // global indices [px_lo, px_hi); runs after the last coded pixel of the band
+  // end at band_next; the band's data starts at bit band_bit0 and shared
+  // output words above zero_floor are zeroed for OR-merging.  Frames: tile
+  // range [0, T), pixels [0, N), band == 0.
+  uint32_t tile_lo, tile_hi;
+  int64_t px_lo, px_hi;
+  uint32_t band;
+  unsigned long long band_next, band_bit0;
 };
 
 __global__ void enc_classify(EncArgs a);
@@ -50,6 +60,10 @@ __global__ void enc_tilebits(EncArgs a);
 __global__ void enc_tilescan(EncArgs a);
 __global__ void enc_pack(EncArgs a);
 __global__ void enc_tail(EncArgs a);
+__global__ void enc_band_edges(EncArgs a, uint32_t* edges);
+__global__ void enc_band_sum(EncArgs a, unsigned long long* info);
+__global__ void enc_band_merge(uint32_t* out32, const uint32_t* words, const unsigned long long* band_w0,
+                               const unsigned long long* band_off, uint32_t R);
 __global__ void enc_serial(EncArgs a);
 
 }  // namespace nice

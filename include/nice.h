@@ -88,6 +88,39 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                           uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
                           uint64_t px_stride, uint32_t flags, int32_t* d_status);
 
+/* ---- one image sharded over ranks (config 4) ----
+ * The image's raster is cut into bands of whole encoder tiles (1024 pixels in
+ * raster order); rank r encodes tiles [tile_lo, tile_hi).  The caller runs the
+ * exchange steps between the calls (bench/tests use RCCL via torch.distributed):
+ *   1. nice_band_classify   band records + d_edges = {first, last} coded pixel
+ *                           (0xFFFFFFFF: none)
+ *   2. all-gather edges     band_next = first coded pixel of the later bands (w*h: none)
+ *      nice_band_runs       the band's symbol histogram (858 x u32) into d_hist
+ *   3. all-reduce (sum)     nice_band_tables: identical code tables on every rank;
+ *                           returns the band's data bits and the data start bit
+ *   4. all-gather bits      band_bit0 = data start + bits of the earlier bands
+ *      nice_band_pack       nice_band_words() words: the band's bits at their
+ *                           stream position (first/last word partial)
+ *   5. gather words         nice_band_assemble (one rank): header + bands + tail
+ * The result equals nice_encode of the whole image byte for byte.  Frames whose
+ * codes exceed 25 bits need the serial writer: nice_band_tables returns
+ * NICE_E_UNSUPPORTED for them.
+ * d_px holds pixels [px0, px0 + px_count) (global raster index), which must
+ * cover the band and the 3 rows + 3 pixels before it. */
+int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t px0, uint64_t px_count,
+                       uint32_t w, uint32_t h, uint8_t channels, uint8_t channels_out, uint32_t tile_lo,
+                       uint32_t tile_hi, uint32_t* d_edges);
+int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_hist);
+int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, uint64_t* band_bits,
+                     uint64_t* seed_bit);
+uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits);
+int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_words, uint64_t words_cap);
+int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, const uint64_t* band_bit0,
+                       const uint64_t* band_bits, uint32_t n_bands, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* out_len);
+/* Encoder tile size (pixels) used by the band API. */
+uint32_t nice_tile_pixels(void);
+
 /* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
 enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,
