@@ -29,19 +29,21 @@ HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
 AMP = [0, 1, 2, 3, 8, 24, 64, 256]
 
 
-def syn_frames(torch, n, W, H, seed0, device):
+def syn_frames(torch, n, W, H, seed0, device, y0=0, y1=None):
     """Photo-like RGBA frames (SYN-v1 structure with a counter-based hash in
     place of the serial xorshift): per-band noise amplitudes 0..256, 1/7 of the
-    16x16 blocks flat, A = 255."""
-    y = torch.arange(H, device=device, dtype=torch.int64).view(H, 1)
+    16x16 blocks flat, A = 255.  Rows [y0, y1) only, if given."""
+    y1 = H if y1 is None else y1
+    y = torch.arange(y0, y1, device=device, dtype=torch.int64).view(y1 - y0, 1)
     x = torch.arange(W, device=device, dtype=torch.int64).view(1, W)
     bx = (200 * x) // max(W - 1, 1)
     by = (200 * y) // max(H - 1, 1)
-    base = [bx.expand(H, W), by.expand(H, W), ((bx + by) // 2)]
+    R = y1 - y0
+    base = [bx.expand(R, W), by.expand(R, W), ((bx + by) // 2)]
     flat = (((x // 16) + (y // 16)) % 7) == 0
-    amp = torch.tensor(AMP, device=device, dtype=torch.int64)[(8 * y) // H].expand(H, W)
+    amp = torch.tensor(AMP, device=device, dtype=torch.int64)[(8 * y) // H].expand(R, W)
     idx = y * W + x
-    out = torch.empty((n, H, W, 4), dtype=torch.uint8, device=device)
+    out = torch.empty((n, R, W, 4), dtype=torch.uint8, device=device)
     M = 0xFFFFFFFF
     for f in range(n):
         for c in range(3):
@@ -58,7 +60,7 @@ def syn_frames(torch, n, W, H, seed0, device):
             fv = [40, 80, 120][c]
             out[f, :, :, c] = torch.where(flat, torch.full_like(val, fv), val).to(torch.uint8)
         out[f, :, :, 3] = 255
-    return out.view(n, H * W * 4)
+    return out.view(n, R * W * 4)
 
 
 def cpu_baseline(W, H, seconds=12.0):
@@ -120,6 +122,31 @@ def load_traffic(kernel, frames, path=None):
         return None
 
 
+def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
+    """BASELINE config 4: one side x side RGBA image encoded by all ranks
+    (bands + RCCL exchanges, fast-losless-image-compression-format_amd/sharded.py)."""
+    S = importlib.import_module(PKG + ".sharded")
+    W = H = side
+    lo, hi = S.band_tiles(W, H, rank, world)
+    p0, p1 = S.band_pixels(W, H, lo, hi)
+    y0, y1 = p0 // W, (p1 + W - 1) // W
+    rows = syn_frames(torch, 1, W, H, 11, device, y0, y1).view(-1)
+    px = rows[(p0 - y0 * W) * 4:(p1 - y0 * W) * 4]
+    be = S.HipBands(device.index or 0)
+    out = S.encode_sharded(be, dist, px, p0, W, H, 4)   # warmup
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = S.encode_sharded(be, dist, px, p0, W, H, 4)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = max_over_ranks((time.perf_counter() - t0) / reps, dist, device)
+    return {"workload": f"1 x {W}x{H} RGBA image, bands over {world} ranks, RCCL exchanges + gather-v",
+            "ms": round(el * 1e3, 3), "mpix_s": round(W * H / el / 1e6, 2),
+            "stream_bytes": int(out.numel()) if out is not None else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +157,8 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sharded-side", type=int, default=16384,
+                    help="N>1: also time one side x side image encoded across the ranks (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -197,6 +226,13 @@ def main():
     t_one = timed(lambda: (nice.encode_batch(one_px, W, H, 4, one_s, one_l),
                            nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st)), reps=2)
 
+    sharded = None
+    if world > 1 and args.sharded_side:
+        try:
+            sharded = sharded_image(torch, nice, dist, device, args.sharded_side, rank, world)
+        except Exception as exc:   # report, never lose the main measurement
+            sharded = {"error": repr(exc)[:300]}
+
     names = [L.nice_phase_name(i).decode() for i in range(32)]
     phase = {names[i]: {"ms_total": round(ms[i], 3), "launches": int(cnt[i])}
              for i in range(32) if cnt[i] and names[i]}
@@ -245,6 +281,7 @@ def main():
         "stream_bytes_per_frame": stream_bytes // F,
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,
+        "sharded_image_encode": sharded,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
