@@ -26,7 +26,7 @@ from dataclasses import dataclass
 __all__ = [
     "Image", "encode", "decode", "encode_bytes", "decode_bytes", "encode_bound",
     "encode_batch", "decode_batch", "NiceError", "lib", "LIB_PATH",
-    "DEC_STRICT_REFERENCE", "DEC_ALPHA_FILL_FF",
+    "DEC_STRICT_REFERENCE", "DEC_ALPHA_FILL_FF", "DEC_TOLERANT_HEADER",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,6 +39,7 @@ _ERRNAMES = {E_ARG: "bad argument", E_HIP: "HIP runtime failure", E_NODEV: "no g
              E_UNSUPPORTED: "stream outside the reference decoder's domain"}
 DEC_STRICT_REFERENCE = 0x1
 DEC_ALPHA_FILL_FF = 0x2
+DEC_TOLERANT_HEADER = 0x4   # repair spilled 5-bit max fields (small / flat images)
 
 EXPORTS = [
     "nice_version", "nice_device_count", "nice_encode_bound", "nice_encode", "nice_peek_header",

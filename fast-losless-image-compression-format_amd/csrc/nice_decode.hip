@@ -88,8 +88,47 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
       lens[stream_base(st) + i] = (uint8_t)(src.peek32(pos + 7u * i) >> 25);
   }
   __syncthreads();
-  // validity: every length in [1, max], max attained, Kraft sum == 1
-  if (threadIdx.x < N_STREAMS) {
+  const bool tolerant = (a.flags & NICE_DEC_TOLERANT_HEADER) && !(a.flags & NICE_DEC_STRICT_REFERENCE);
+  if (tolerant) {
+    // Spilled max fields (oracle tolerant_tables): a max above 31
+    // keeps its low 5 bits in the field and adds max >> 5 into the p bits still
+    // pending in the writer's u32 cache -- the low p bits of the previous
+    // stream's last length, p = table-header bits written so far mod 8.  Undo it
+    // from the last stream down; the table max becomes the longest decodable
+    // (<= 31 bit) length.
+    if (threadIdx.x == 0) {
+      for (int st = N_STREAMS - 1; st >= 0; --st) {
+        const int n = stream_size(st), b = stream_base(st);
+        uint32_t mx = 0, dm = 0;
+        for (int i = 0; i < n; ++i) {
+          const uint32_t l = lens[b + i];
+          mx = max(mx, l);
+          if (l <= 31) dm = max(dm, l);
+        }
+        if ((mx & 31u) != smax[st] || mx > 127 || dm == 0) bad = 1;
+        if (mx >= 32 && st > 0) {
+          uint32_t bits = 0;
+          for (int q = 0; q < st; ++q) bits += 5u + 7u * (uint32_t)stream_size(q);
+          const uint32_t pm = (1u << (bits & 7u)) - 1u;
+          uint8_t& last = lens[stream_base(st - 1) + stream_size(st - 1) - 1];
+          last = (uint8_t)((last & ~pm) | ((last - (mx >> 5)) & pm));
+        }
+        smax[st] = (uint8_t)dm;
+      }
+    }
+    __syncthreads();
+    // every stream a complete prefix code over all its lengths (Kraft sum 1)
+    if (threadIdx.x < N_STREAMS) {
+      const int st = threadIdx.x, n = stream_size(st), b = stream_base(st);
+      uint32_t mx = 0;
+      bool ok = true;
+      for (int i = 0; i < n; ++i) { mx = max(mx, (uint32_t)lens[b + i]); ok = ok && lens[b + i] >= 1; }
+      unsigned __int128 kraft = 0;
+      for (int i = 0; i < n && ok; ++i) kraft += (unsigned __int128)1 << (mx - lens[b + i]);
+      if (!ok || kraft != ((unsigned __int128)1 << mx)) atomicOr(&bad, 1);
+    }
+  } else if (threadIdx.x < N_STREAMS) {
+    // validity: every length in [1, max], max attained, Kraft sum == 1
     const int st = threadIdx.x;
     const uint32_t mx = smax[st];
     uint64_t kraft = 0;
@@ -153,26 +192,43 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     T->max_aob[st] = (uint8_t)mx;
     T->lut_bits[st] = (uint8_t)lb;
     T->lut_off[st] = loff[st];
+    // hfe.rs:271-290 with usize wrapping (shift amounts masked to 6 bits); in
+    // tolerant mode lengths above 31 (zero-count symbols) get no decode entry
+    // (lo above every 31-bit window value) and the decodable codes must fit
+    // their lengths and not overlap
     unsigned long long cur = 0;
     uint32_t prev = 0;
+    uint64_t prev_lo = ~0ull;
+    bool ok = true;
     for (int k = 0; k < n; ++k) {
       const int sym = order[b + k];
       const uint32_t l = lens[b + sym];
-      if (l < prev) cur >>= (prev - l);
+      if (l < prev) cur >>= (prev - l) & 63u;
       if (prev > 0) cur += 1;
-      const uint32_t code = (uint32_t)((1ull << l) - cur - 1ull);
+      const unsigned long long code64 = (1ull << (l & 63u)) - cur - 1ull;
       prev = l;
-      T->lo[b + k] = code << (mx - l);
       T->sym[b + k] = (uint16_t)sym;
       T->len[b + k] = (uint8_t)l;
+      if (l > mx) { T->lo[b + k] = 0xFFFFFFFFu; continue; }
+      const uint32_t code = (uint32_t)code64;
+      const uint64_t lo = (uint64_t)code << (mx - l);
+      if ((code64 >> l) != 0 || (prev_lo != ~0ull && lo + (1ull << (mx - l)) > prev_lo)) ok = false;
+      prev_lo = lo;
+      T->lo[b + k] = (uint32_t)lo;
       // first-level entries
       if (l <= lb) {
         const uint32_t e0 = code << (lb - l), e1 = (code + 1) << (lb - l);
-        for (uint32_t e = e0; e < e1; ++e) lut[e] = (uint16_t)((sym << 5) | l);
+        for (uint32_t e = e0; e < e1 && e < (1u << lb); ++e) lut[e] = (uint16_t)((sym << 5) | l);
       } else {
         lut[code >> (l - lb)] = 0;   // long-code marker
       }
     }
+    if (!ok) atomicOr(&bad, 1);
+  }
+  __syncthreads();
+  if (bad) {
+    if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_UNSUPPORTED);
+    return;
   }
   if (threadIdx.x == 0) a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
 }

@@ -37,6 +37,13 @@ enum {
 /* nice_decode flags */
 #define NICE_DEC_STRICT_REFERENCE 0x1u /* fail wherever the reference decoder would fail */
 #define NICE_DEC_ALPHA_FILL_FF 0x2u    /* 4-channel output: write A = 255 */
+/* Tolerant table header: repairs the length field a
+ * spilled 5-bit max (> 31) corrupts in the reference writer, and decodes with
+ * the <= 31-bit codes.  Streams of small or very flat images (every max > 31
+ * because zero-count symbols chain deep in the Huffman merge) decode only
+ * with this flag; the reference decoder cannot decode them.  Ignored with
+ * NICE_DEC_STRICT_REFERENCE. */
+#define NICE_DEC_TOLERANT_HEADER 0x4u
 
 typedef struct nice_ctx nice_ctx;
 

@@ -489,7 +489,11 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
 /* stride everywhere (the evident intent), used only to check RGBA round trips.*/
 /* ------------------------------------------------------------------------- */
 typedef struct { uint16_t symbol; uint8_t aob; } lut_t;
-typedef struct { uint8_t max_aob; lut_t *lut; size_t lut_len; } sslookup_t;
+typedef struct {
+    uint8_t max_aob; lut_t *lut; size_t lut_len;
+    /* tolerant tables (canonical order, decodable entries only) */
+    int ncanon; uint32_t *clo; uint16_t *csym; uint8_t *clen;
+} sslookup_t;
 
 static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
     uint8_t mx;
@@ -533,6 +537,95 @@ static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
     return rc;
 }
 
+/* Tolerant tables (NICE_ORACLE_DEC_TOLERANT).  The
+ * writer puts each stream's max length into a 5-bit field with
+ * `cache += v << (32 - k)` (hfe.rs:97-99, bitwriter.rs:17-35): a max above 31
+ * keeps its low 5 bits in the field and ADDS `max >> 5` into the bits before it
+ * that are still pending in the u32 cache: the low p bits of the previous
+ * stream's last 7-bit length, p = (bits written so far) mod 8 (write_8bits
+ * flushes one byte per call, so at most 7 bits are pending); carries out of
+ * them fall off the top of the cache, as does all of stream 0's spill.
+ * Repair, from the last stream down: the true max of stream t is the max of its
+ * 7-bit lengths (its own last entry already repaired); it must agree with the
+ * field mod 32; if it is >= 32, subtract the spill from those p bits mod 2^p.  Each stream must then
+ * be a complete prefix code (Kraft sum exactly 1, 128-bit exact).  Codes follow
+ * amount_of_bits_to_bcodes (hfe.rs:255-296) with usize wrapping; only lengths
+ * <= 31 are decodable (longer ones are the zero-count symbols the Huffman
+ * merge pushes deep), and the decodable codes must not overlap. */
+static int tolerant_tables(bitreader_t *r, sslookup_t *L) {
+    uint8_t field[N_STREAMS];
+    uint8_t *a[N_STREAMS];
+    int rc = 0;
+    for (int t = 0; t < N_STREAMS; ++t) a[t] = NULL;
+    for (int t = 0; t < N_STREAMS && !rc; ++t) {
+        if (br_read_bitsu8(r, 5, &field[t])) { rc = NICE_ORACLE_E_PANIC; break; }
+        uint8_t fb = field_bits(field[t]);            /* 7 for every 5-bit value */
+        a[t] = (uint8_t *)malloc((size_t)STREAM_N[t]);
+        for (int i = 0; i < STREAM_N[t]; ++i)
+            if (br_read_bitsu8(r, fb, &a[t][i])) { rc = NICE_ORACLE_E_PANIC; break; }
+    }
+    for (int t = N_STREAMS - 1; t >= 0 && !rc; --t) {
+        unsigned mx = 0;
+        for (int i = 0; i < STREAM_N[t]; ++i) if (a[t][i] > mx) mx = a[t][i];
+        if ((mx & 31u) != field[t] || mx > 127) { rc = NICE_ORACLE_E_DOMAIN; break; }
+        if (mx >= 32 && t > 0) {
+            /* the spill lands in the p bits still pending in the writer's cache
+             * (the low p bits of the previous field, p = bits written mod 8);
+             * carries out of them leave the u32 cache */
+            unsigned bits = 0;
+            for (int q = 0; q < t; ++q) bits += 5u + 7u * (unsigned)STREAM_N[q];
+            const unsigned p = bits & 7u, m = (1u << p) - 1u;
+            uint8_t *last = &a[t - 1][STREAM_N[t - 1] - 1];
+            *last = (uint8_t)((*last & ~m) | ((*last - (mx >> 5)) & m));
+        }
+    }
+    for (int t = 0; t < N_STREAMS && !rc; ++t) {
+        const int n = STREAM_N[t];
+        unsigned mx = 0, dm = 0;
+        unsigned __int128 kraft = 0;
+        for (int i = 0; i < n; ++i) {
+            if (a[t][i] < 1) { rc = NICE_ORACLE_E_DOMAIN; break; }
+            if (a[t][i] > mx) mx = a[t][i];
+            if (a[t][i] <= 31 && a[t][i] > dm) dm = a[t][i];
+        }
+        if (rc) break;
+        for (int i = 0; i < n; ++i) kraft += (unsigned __int128)1 << (mx - a[t][i]);
+        if (kraft != ((unsigned __int128)1 << mx) || dm == 0) { rc = NICE_ORACLE_E_DOMAIN; break; }
+        uint64_t *code = (uint64_t *)malloc(8 * (size_t)n);
+        nice_oracle_canonical(a[t], n, code);
+        sslookup_t *sl = &L[t];
+        sl->max_aob = (uint8_t)dm;
+        sl->clo = (uint32_t *)malloc(4 * (size_t)n);
+        sl->csym = (uint16_t *)malloc(2 * (size_t)n);
+        sl->clen = (uint8_t *)malloc((size_t)n);
+        sl->ncanon = 0;
+        /* decodable entries in canonical order: (length desc, symbol desc) */
+        for (unsigned l = dm; l >= 1; --l)
+            for (int i = n - 1; i >= 0; --i)
+                if (a[t][i] == l) {
+                    if (code[i] >> l) { rc = NICE_ORACLE_E_DOMAIN; break; }
+                    int k = sl->ncanon++;
+                    sl->clo[k] = (uint32_t)(code[i] << (dm - l));
+                    sl->csym[k] = (uint16_t)i;
+                    sl->clen[k] = (uint8_t)l;
+                    /* intervals [lo, lo + 2^(dm-l)) descend without overlap */
+                    if (k > 0 && (uint64_t)sl->clo[k] + ((uint64_t)1 << (dm - l)) > sl->clo[k - 1])
+                        rc = NICE_ORACLE_E_DOMAIN;
+                }
+        free(code);
+    }
+    for (int t = 0; t < N_STREAMS; ++t) free(a[t]);
+    return rc;
+}
+
+static int canon_lookup(const sslookup_t *sl, uint32_t v, unsigned *sym, uint8_t *len) {
+    for (int k = sl->ncanon - 1; k >= 0; --k) {           /* shortest (lowest) codes first */
+        uint64_t span = (uint64_t)1 << (sl->max_aob - sl->clen[k]);
+        if (v >= sl->clo[k] && v < sl->clo[k] + span) { *sym = sl->csym[k]; *len = sl->clen[k]; return 0; }
+    }
+    return NICE_ORACLE_E_PANIC;                             /* bits match no decodable code */
+}
+
 /* Absolute-position reader with the same byte semantics (bytes past the end
  * read as the last stream byte) but no u32 cache: what the reference reader
  * computes whenever it terminates.  Used by NICE_ORACLE_DEC_STRIDE ("intent"). */
@@ -556,6 +649,13 @@ typedef struct {
 
 static inline int read_next_symbol_x(symreader_t *sr, const sslookup_t *sl, unsigned *sym) {
     uint32_t v;
+    if (sl->clo) {                                       /* tolerant tables */
+        uint8_t l8;
+        int e = canon_lookup(sl, abs_peek(sr->r.p, sr->r.len, sr->bitpos, sl->max_aob), sym, &l8);
+        if (e) return e;
+        sr->bitpos += l8;
+        return 0;
+    }
     if (sr->intent) {
         v = abs_peek(sr->r.p, sr->r.len, sr->bitpos, sl->max_aob);
     } else {
@@ -612,13 +712,14 @@ int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, si
     sslookup_t L[N_STREAMS];
     memset(L, 0, sizeof(L));
     int rc = 0;
-    for (int k = 0; k < N_STREAMS && !rc; ++k) rc = read_header_into_tree(&r, &L[k], STREAM_N[k]);
+    if (mode == NICE_ORACLE_DEC_TOLERANT) rc = tolerant_tables(&r, L);
+    else for (int k = 0; k < N_STREAMS && !rc; ++k) rc = read_header_into_tree(&r, &L[k], STREAM_N[k]);
     const size_t rel_ref[11] = {ch, ch * W, ch * (W - 1), ch * (W - 3), 3 * ch,
                                 ch * (3 * W - 1), 3 * ch * W, ch * (3 * W + 1), ch * (W + 3),
                                 ch * 3 * (W + 1), ch * 3 * (W - 1)};
     const size_t back_ref[5] = {ch, ch * W, ch * (W - 1), 2 * ch, 2 * ch * W};
     const size_t rowb = ch * W;
-    const int intent = (mode == NICE_ORACLE_DEC_STRIDE);
+    const int intent = (mode == NICE_ORACLE_DEC_STRIDE || mode == NICE_ORACLE_DEC_TOLERANT);
     const size_t step = intent ? ch : 3;                                /* code.rs:659 */
     symreader_t sr;
     sr.r = r; sr.intent = intent;
@@ -734,7 +835,7 @@ int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, si
     }
     (void)v;
 done:
-    for (int k = 0; k < N_STREAMS; ++k) free(L[k].lut);
+    for (int k = 0; k < N_STREAMS; ++k) { free(L[k].lut); free(L[k].clo); free(L[k].csym); free(L[k].clen); }
     if (rc) { free(o); return rc; }
     *out = o;
     *out_len = image_size;

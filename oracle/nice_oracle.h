@@ -19,7 +19,9 @@ enum {
     NICE_ORACLE_E_HANG = -5    /* the reference decoder would loop forever (bitreader.rs:88-97 u8 wrap) */
 };
 
-enum { NICE_ORACLE_DEC_REFERENCE = 0, NICE_ORACLE_DEC_STRIDE = 1 };
+/* DEC_STRIDE: pixel stride = channels (intent); DEC_TOLERANT: DEC_STRIDE plus the
+ * tolerant table header of SURVEY.md Appendix A.5 (spilled max fields repaired). */
+enum { NICE_ORACLE_DEC_REFERENCE = 0, NICE_ORACLE_DEC_STRIDE = 1, NICE_ORACLE_DEC_TOLERANT = 2 };
 
 typedef struct {
     uint8_t max_aob[10];       /* per-stream max code length (hfe.rs:97) */

@@ -19,6 +19,7 @@ _lib = None
 STREAM_N = [256, 13, 64, 32, 11, 343, 64, 32, 32, 11]
 DEC_REFERENCE = 0
 DEC_STRIDE = 1          # "intent" decode: pixel stride = channels, correct bit reader
+DEC_TOLERANT = 2        # DEC_STRIDE + tolerant table header (spilled max fields repaired)
 E_PANIC, E_DOMAIN, E_HANG = -3, -4, -5
 
 
