@@ -25,7 +25,7 @@ from dataclasses import dataclass
 
 __all__ = [
     "Image", "encode", "decode", "encode_bytes", "decode_bytes", "encode_bound",
-    "encode_batch", "decode_batch", "NiceError", "lib", "LIB_PATH",
+    "encode_batch", "decode_batch", "Pipeline", "NiceError", "lib", "LIB_PATH",
     "DEC_STRICT_REFERENCE", "DEC_ALPHA_FILL_FF", "DEC_TOLERANT_HEADER",
 ]
 
@@ -47,6 +47,8 @@ EXPORTS = [
     "nice_encode_batch_dev", "nice_decode_batch_dev",
     "nice_band_classify", "nice_band_runs", "nice_band_tables", "nice_band_words", "nice_band_pack",
     "nice_band_assemble", "nice_tile_pixels",
+    "nice_pipe_create", "nice_pipe_destroy", "nice_pipe_stream_stride", "nice_pipe_encode",
+    "nice_pipe_decode",
 ]
 
 
@@ -93,6 +95,15 @@ def lib():
                                         ctypes.c_uint8, ctypes.c_uint8, u8p, u64, u8p]
     L.nice_decode_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u64, u8p, u32, u32,
                                         u32, ctypes.c_uint8, u8p, u64, u32, u8p]
+    L.nice_pipe_create.argtypes = [ctypes.c_int, u32, u32, ctypes.c_uint8, u32, u32,
+                                   ctypes.POINTER(ctypes.c_void_p)]
+    L.nice_pipe_destroy.argtypes = [ctypes.c_void_p]
+    L.nice_pipe_stream_stride.restype = u64
+    L.nice_pipe_stream_stride.argtypes = [ctypes.c_void_p]
+    L.nice_pipe_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u32, ctypes.c_uint8,
+                                   ctypes.c_void_p, u64, ctypes.c_void_p]
+    L.nice_pipe_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u32,
+                                   ctypes.c_uint8, ctypes.c_void_p, u32, ctypes.c_void_p]
     _lib = L
     return L
 
@@ -236,3 +247,65 @@ def decode_batch(streams, stream_len, width: int, height: int, out_channels: int
         ctypes.c_void_p(stream_len.data_ptr()), n, width, height, out_channels,
         ctypes.c_void_p(px.data_ptr()), px.stride(0), flags, ctypes.c_void_p(status.data_ptr()))
     _check(rc, "nice_decode_batch_dev")
+
+
+# ---- streamed host pipeline (config 5: H2D / compute / D2H overlapped) ------
+def _host_ptr(buf):
+    """Address of a host buffer: numpy array, bytearray or CPU torch tensor."""
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    return ctypes.addressof((ctypes.c_uint8 * len(buf)).from_buffer(buf))
+
+
+class Pipeline:
+    """Streamed encode/decode of host frames (include/nice.h ``nice_pipe_*``):
+    ``depth`` slots of ``batch`` frames, each with its own HIP stream, so H2D
+    copies, kernels and D2H copies of different slots overlap.  Host buffers
+    may be pinned (``torch.empty(..., pin_memory=True)``: asynchronous copies)
+    or pageable (numpy / bytearray)."""
+
+    def __init__(self, width: int, height: int, channels: int, batch: int = 16, depth: int = 3,
+                 device: int = 0):
+        self.width, self.height, self.channels = width, height, channels
+        self.ptr = ctypes.c_void_p()
+        _check(lib().nice_pipe_create(device, width, height, channels, batch, depth,
+                                      ctypes.byref(self.ptr)), "nice_pipe_create")
+        self.stream_stride = int(lib().nice_pipe_stream_stride(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            lib().nice_pipe_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode(self, frames, outs, channels_out: int | None = None):
+        """frames[f] -> outs[f] (host buffers of >= stream_stride bytes); returns
+        the stream lengths."""
+        n = len(frames)
+        src = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(f) for f in frames])
+        dst = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(o) for o in outs])
+        caps = [o.numel() if hasattr(o, "numel") else len(o) for o in outs]
+        lens = (ctypes.c_uint64 * max(n, 1))()
+        co = self.channels if channels_out is None else channels_out
+        _check(lib().nice_pipe_encode(self.ptr, src, n, co, dst, min(caps) if caps else 0, lens),
+               "nice_pipe_encode")
+        return [int(lens[i]) for i in range(n)]
+
+    def decode(self, streams, lengths, outs, out_channels: int | None = None,
+               flags: int = DEC_ALPHA_FILL_FF):
+        """streams[f] (lengths[f] bytes) -> outs[f] (W*H*out_channels bytes)."""
+        n = len(streams)
+        src = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(s) for s in streams])
+        dst = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(o) for o in outs])
+        ln = (ctypes.c_uint64 * max(n, 1))(*lengths)
+        status = (ctypes.c_int32 * max(n, 1))()
+        oc = self.channels if out_channels is None else out_channels
+        _check(lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status), "nice_pipe_decode")
+        return [int(status[i]) for i in range(n)]

@@ -14,6 +14,7 @@
 #include "nice_format.h"
 #include "nice_bits.hpp"
 #include "nice_kernels.h"
+#include "nice_internal.h"
 
 using namespace nice;
 
@@ -330,6 +331,9 @@ struct DecLayout {
   size_t total;
   size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
 };
+// Jacobi iterations queued before the host first checks for the fixpoint (one
+// change flag each); further iterations, if any, check after every launch.
+constexpr uint32_t kSyncQueued = 6, kSyncFlags = 8;
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf) {
   DecLayout L{};
   size_t o = 0;
@@ -342,7 +346,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_cpx = take((size_t)n_frames * max_chunks * 8);
   L.o_cstart = take((size_t)n_frames * max_chunks * 8);
   L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
-  L.o_changed = take(16);
+  L.o_changed = take(4 * kSyncFlags);
   L.o_rowbuf = take(rowbuf);
   L.total = o;
   return L;
@@ -424,6 +428,18 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                           uint64_t stream_stride, const uint64_t* d_stream_len, uint32_t n_frames,
                           uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
                           uint64_t px_stride, uint32_t flags, int32_t* d_status) {
+  return nice::decode_batch_impl(ctx, stream, d_streams, stream_stride, d_stream_len, nullptr, n_frames, w, h,
+                                 out_channels, d_px, px_stride, flags, d_status);
+}
+
+}  // extern "C"
+
+// h_stream_len: the lengths on the host when the caller has them (saves a
+// device round trip), else nullptr.
+int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_streams, uint64_t stream_stride,
+                            const uint64_t* d_stream_len, const uint64_t* h_stream_len, uint32_t n_frames,
+                            uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px, uint64_t px_stride,
+                            uint32_t flags, int32_t* d_status) {
   if (!ctx || !d_streams || !d_stream_len || !d_status) return NICE_E_ARG;
   if (out_channels != 3 && out_channels != 4) return NICE_E_ARG;
   if ((stream_stride & 3) || ((uintptr_t)d_streams & 3)) return NICE_E_ARG;
@@ -436,8 +452,12 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   NICE_HIP(hipMemsetAsync(d_status, 0, (size_t)n_frames * 4, st));
   // stream lengths bound the chunk grid
   std::vector<uint64_t> lens(n_frames);
-  NICE_HIP(hipMemcpyAsync(lens.data(), d_stream_len, (size_t)n_frames * 8, hipMemcpyDeviceToHost, st));
-  NICE_HIP(hipStreamSynchronize(st));
+  if (h_stream_len) {
+    std::copy(h_stream_len, h_stream_len + n_frames, lens.begin());
+  } else {
+    NICE_HIP(hipMemcpyAsync(lens.data(), d_stream_len, (size_t)n_frames * 8, hipMemcpyDeviceToHost, st));
+    NICE_HIP(hipStreamSynchronize(st));
+  }
   uint64_t max_len = 0;
   for (uint64_t l : lens) {
     if (l > stream_stride) return NICE_E_ARG;
@@ -521,14 +541,26 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                      dim3(256), 0, st, a);
   const dim3 cgrid(n_frames * a.chunk_blocks);
   // Jacobi iteration of the chunk entry states to the fixpoint
+  // (the first kSyncQueued launches go out without host round trips: each one
+  // returns at once if the previous one changed nothing)
   uint32_t host_changed = 1;
   uint32_t it_count = 0;
-  for (uint32_t it = 0; host_changed && it < max_chunks + 2; ++it, ++it_count) {
-    NICE_HIP(hipMemsetAsync(changed, 0, 4, st));
+  const uint32_t max_it = max_chunks + 2;
+  const uint32_t queued = std::min(kSyncQueued, max_it);
+  NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
+  for (uint32_t it = 0; it < queued; ++it, ++it_count) {
     tm.begin(NICE_PH_DEC_SYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
     tm.end(st);
-    NICE_HIP(hipMemcpyAsync(&host_changed, changed, 4, hipMemcpyDeviceToHost, st));
+  }
+  NICE_HIP(hipMemcpyAsync(&host_changed, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
+  NICE_HIP(hipStreamSynchronize(st));
+  for (uint32_t it = queued; host_changed && it < max_it; ++it, ++it_count) {
+    NICE_HIP(hipMemsetAsync(changed + kSyncFlags - 1, 0, 4, st));
+    tm.begin(NICE_PH_DEC_SYNC, st);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed + kSyncFlags - 1, nullptr);
+    tm.end(st);
+    NICE_HIP(hipMemcpyAsync(&host_changed, changed + kSyncFlags - 1, 4, hipMemcpyDeviceToHost, st));
     NICE_HIP(hipStreamSynchronize(st));
   }
   // the last sync iteration (no entry changed) already produced chunk_px
@@ -575,6 +607,8 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }
+
+extern "C" {
 
 // ---- one image sharded over ranks ------------------------
 int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t px0, uint64_t px_count,

@@ -452,9 +452,13 @@ __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
 // CK_BITS; once they agree the rest of the slice is unchanged (Huffman
 // self-synchronisation), so the lane stops and only patches its pixel count.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed) {
+// `prev`: the previous iteration's change flag -- when it is 0 the entries are
+// at the fixpoint already and this launch does nothing (the host queues several
+// iterations without waiting for each).
+__global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
+  if (prev && *prev == 0) return;
   const uint32_t f = blockIdx.x / a.chunk_blocks;
   const uint32_t jb = blockIdx.x % a.chunk_blocks;
   if (a.status[f] != 0) return;

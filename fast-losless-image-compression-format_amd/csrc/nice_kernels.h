@@ -106,7 +106,7 @@ struct DecArgs {
 
 __global__ void dec_tables(DecArgs a);
 __global__ void dec_init_entries(DecArgs a);
-__global__ void dec_sync(DecArgs a, uint32_t* changed);
+__global__ void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev);
 __global__ void dec_scan(DecArgs a);
 __global__ void dec_emit(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);

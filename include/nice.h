@@ -128,6 +128,28 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
 /* Encoder tile size (pixels) used by the band API. */
 uint32_t nice_tile_pixels(void);
 
+/* ---- streamed host pipeline (BASELINE config 5) ----
+ * Frames in host memory flow through `depth` slots of `batch` frames; each slot
+ * has its own HIP stream, scratch and device buffers, so one slot's H2D copy,
+ * another's kernels and a third's D2H copy overlap.  Replaces calling
+ * code::encode / code::decode (code.rs:59-64, 464-468) once per image from host
+ * memory (main.rs:28-103).  Host buffers may be pinned (copies asynchronous) or
+ * pageable.  Frames are w x h with `channels` bytes per pixel (fixed per pipe). */
+typedef struct nice_pipe nice_pipe;
+int nice_pipe_create(int device, uint32_t w, uint32_t h, uint8_t channels, uint32_t batch, uint32_t depth,
+                     nice_pipe** out);
+void nice_pipe_destroy(nice_pipe* p);
+/* Bytes per stream slot on the device (>= nice_encode_bound(w, h)). */
+uint64_t nice_pipe_stream_stride(const nice_pipe* p);
+/* px[f]: frame f (w*h*channels bytes).  out[f]: stream f (out_cap bytes
+ * available), out_len[f] its length.  Blocks until every stream is on the host. */
+int nice_pipe_encode(nice_pipe* p, const uint8_t* const* px, uint32_t n_frames, uint8_t channels_out,
+                     uint8_t* const* out, uint64_t out_cap, uint64_t* out_len);
+/* streams[f], stream_len[f] -> px[f] (w*h*out_channels bytes, out_channels <=
+ * the pipe's channels); status[f] per frame (flags as nice_decode).  Blocks. */
+int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, const uint64_t* stream_len, uint32_t n_frames,
+                     uint8_t out_channels, uint8_t* const* px, uint32_t flags, int32_t* status);
+
 /* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
 enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,

@@ -1,0 +1,60 @@
+"""Streamed host pipeline (BASELINE config 5): host
+frames -> H2D -> encode -> D2H streams, and back, overlapped over HIP streams.
+Parity: every stream equals the oracle's code::encode output byte for byte, and
+every decoded frame equals the input, for pinned and pageable host buffers,
+ragged last chunks and depth 1..3."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(O, n, w, h, c, seed0=1):
+    return [O.gen_syn_v1(w, h, c, seed0 + i) for i in range(n)]
+
+
+@pytest.mark.parametrize("batch,depth", [(3, 2), (4, 1), (2, 3), (16, 3)])
+def test_pipe_encode_decode_pageable(nice, O, batch, depth):
+    w, h, c, n = 160, 96, 4, 7
+    frames = _frames(O, n, w, h, c)
+    p = nice.Pipeline(w, h, c, batch=batch, depth=depth)
+    outs = [np.zeros(p.stream_stride, np.uint8) for _ in range(n)]
+    lens = p.encode(frames, outs)
+    for i in range(n):
+        assert outs[i][:lens[i]].tobytes() == O.encode(frames[i], w, h, c), i
+    dec = [np.zeros(w * h * c, np.uint8) for _ in range(n)]
+    st = p.decode(outs, lens, dec)
+    assert st == [0] * n
+    for i in range(n):
+        assert np.array_equal(dec[i].reshape(-1, c)[:, :3], frames[i].reshape(-1, c)[:, :3]), i
+        assert (dec[i].reshape(-1, c)[:, 3] == 255).all()
+    p.close()
+
+
+def test_pipe_pinned_rgb(nice, O):
+    import torch
+    w, h, c, n = 333, 77, 3, 9
+    frames = _frames(O, n, w, h, c, seed0=20)
+    p = nice.Pipeline(w, h, c, batch=4, depth=3)
+    src = [torch.from_numpy(f).pin_memory() for f in frames]
+    outs = [torch.zeros(p.stream_stride, dtype=torch.uint8).pin_memory() for _ in range(n)]
+    lens = p.encode(src, outs)
+    for i in range(n):
+        assert outs[i][:lens[i]].numpy().tobytes() == O.encode(frames[i], w, h, c), i
+    dec = [torch.zeros(w * h * c, dtype=torch.uint8).pin_memory() for _ in range(n)]
+    assert p.decode(outs, lens, dec) == [0] * n
+    for i in range(n):
+        assert np.array_equal(dec[i].numpy(), frames[i]), i
+
+
+def test_pipe_bad_stream_status(nice, O):
+    w, h, c = 64, 64, 3
+    f = O.gen_syn_v1(w, h, c, 3)
+    p = nice.Pipeline(w, h, c, batch=2, depth=2)
+    good = np.frombuffer(O.encode(f, w, h, c), np.uint8).copy()
+    bad = good.copy()
+    bad[4:8] = [0, 0, 0, 9]            # wrong width for this pipe
+    outs = [np.zeros(w * h * c, np.uint8) for _ in range(2)]
+    with pytest.raises(nice.NiceError):
+        p.decode([good, bad], [good.size, bad.size], outs)
+    assert np.array_equal(outs[0], f)
