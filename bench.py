@@ -147,6 +147,51 @@ def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
             "stream_bytes": int(out.numel()) if out is not None else None}
 
 
+def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=16, batch=16, depth=3):
+    """BASELINE config 5: `total` 4K RGBA frames streamed from host memory over
+    the ranks (total / world each): H2D -> encode -> D2H streams, then H2D
+    streams -> decode -> D2H pixels, overlapped over `depth` HIP streams
+    (nice_pipe_*).  Host buffers are pinned; the frame list cycles over
+    `distinct` of them (every frame is still copied and coded in full)."""
+    n = total // world
+    N = W * H
+    k = min(distinct, px.shape[0])
+    src = [px[i].cpu().pin_memory() for i in range(k)]
+    p = nice.Pipeline(W, H, 4, batch=batch, depth=depth, device=device.index or 0)
+    outs = [torch.empty(p.stream_stride, dtype=torch.uint8).pin_memory() for _ in range(k)]
+    dec = [torch.empty(N * 4, dtype=torch.uint8).pin_memory() for _ in range(k)]
+    frames = [src[i % k] for i in range(n)]
+    o_list = [outs[i % k] for i in range(n)]
+    d_list = [dec[i % k] for i in range(n)]
+    warm = min(n, 2 * batch)
+    lens = p.encode(frames[:warm], o_list[:warm])
+    p.decode(o_list[:warm], lens, d_list[:warm])
+    for i in range(k):
+        assert torch.equal(dec[i].view(N, 4)[:, :3], src[i].view(N, 4)[:, :3]), "streamed round trip"
+    barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
+    barrier()
+    t0 = time.perf_counter()
+    lens = p.encode(frames, o_list)
+    t_enc = time.perf_counter() - t0
+    barrier()
+    t1 = time.perf_counter()
+    st = p.decode(o_list, lens, d_list)
+    t_dec = time.perf_counter() - t1
+    assert st == [0] * n
+    t_enc = max_over_ranks(t_enc, dist, device)
+    t_dec = max_over_ranks(t_dec, dist, device)
+    p.close()
+    px_all = n * world * N
+    sb = sum(lens[:k]) / k
+    return {"workload": f"{n * world} x {W}x{H} RGBA frames from pinned host memory, {n} per GPU, "
+                        f"H2D/compute/D2H overlapped ({depth} slots x {batch} frames)",
+            "encode_mpix_s": round(px_all / t_enc / 1e6, 2),
+            "decode_mpix_s": round(px_all / t_dec / 1e6, 2),
+            "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
+            "pcie_gb_s_per_gpu": {"encode": round(n * (N * 4 + sb) / t_enc / 1e9, 2),
+                                  "decode": round(n * (N * 4 + sb) / t_dec / 1e9, 2)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +202,8 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--streamed-frames", type=int, default=1024,
+                    help="config 5: frames streamed from host memory over all ranks (0: skip)")
     ap.add_argument("--sharded-side", type=int, default=16384,
                     help="N>1: also time one side x side image encoded across the ranks (0: skip)")
     args = ap.parse_args()
@@ -233,6 +280,13 @@ def main():
         except Exception as exc:   # report, never lose the main measurement
             sharded = {"error": repr(exc)[:300]}
 
+    stream_leg = None
+    if args.streamed_frames:
+        try:
+            stream_leg = streamed(torch, nice, dist, device, px, W, H, rank, world, args.streamed_frames)
+        except Exception as exc:   # report, never lose the main measurement
+            stream_leg = {"error": repr(exc)[:300]}
+
     names = [L.nice_phase_name(i).decode() for i in range(32)]
     phase = {names[i]: {"ms_total": round(ms[i], 3), "launches": int(cnt[i])}
              for i in range(32) if cnt[i] and names[i]}
@@ -282,6 +336,7 @@ def main():
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,
         "sharded_image_encode": sharded,
+        "streamed_host_frames": stream_leg,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

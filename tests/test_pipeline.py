@@ -48,7 +48,7 @@ def test_pipe_pinned_rgb(nice, O):
 
 
 def test_pipe_bad_stream_status(nice, O):
-    w, h, c = 64, 64, 3
+    w, h, c = 160, 120, 3
     f = O.gen_syn_v1(w, h, c, 3)
     p = nice.Pipeline(w, h, c, batch=2, depth=2)
     good = np.frombuffer(O.encode(f, w, h, c), np.uint8).copy()
