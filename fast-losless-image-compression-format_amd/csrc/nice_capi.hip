@@ -282,14 +282,19 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   if (T > 0) {
     // contiguous tile chunks per block: keeps rows-above reuse in L2 and
     // flushes each block's LDS histogram once per frame
-    uint64_t blocks = 2048;
+    // RGBA frames: ring-staged kernel (each pixel loaded once; >= 16 tiles per
+    // block so the 3-row prefill is amortised, 2 blocks per CU)
+    const bool ring = channels == 4 && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
+    uint64_t blocks = ring ? 512 : 2048;
     uint64_t per = (total_tiles + blocks - 1) / blocks;
-    if (per < 1) per = 1;
+    if (per < (ring ? 16u : 1u)) per = ring ? 16 : 1;
+    if (ring && per > 16384) per = 16384;   // its 16-bit per-thread prefix counters
     blocks = (total_tiles + per - 1) / per;
     a.tiles_per_block = (uint32_t)per;
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
-    hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    if (ring) hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
     hipLaunchKernelGGL(enc_tailruns, dim3(n_frames), dim3(1024), 0, st, a);

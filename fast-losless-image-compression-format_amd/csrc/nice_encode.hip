@@ -331,6 +331,238 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// K1r: classify, ring-staged (RGBA frames, 3 <= W <= CLS_RING_MAX_W).
+//
+// Same outputs as enc_classify (records, histogram, tile first/last coded
+// pixel), restructured for the instruction budget:
+//  * every pixel is loaded from HBM and converted once: a block walks its tile
+//    range in raster order and keeps the last CLS_RING pixels (>= 3 rows + 3 px
+//    + one tile) in an LDS ring indexed by pixel & (CLS_RING - 1); the next
+//    tile is loaded into registers while the current one is classified;
+//  * pixels are held in "luma space", Y = (R-G) | G << 10 | (B-G) << 20 (each
+//    field mod 256).  The transform is a bijection, so the equality tests of
+//    back references and runs hold unchanged, and the luma test of code.rs:
+//    296-336 against reference pixel R -- g = XG-RG in [-32,32), XR-RR-g and
+//    XB-RB-g in [-16,16) -- becomes a range test on the field-wise difference
+//    Y(X) - Y(R): one subtract, one AND, one compare per reference;
+//  * the five mode-prefix counts are accumulated per thread in packed
+//    registers and added to the histogram once per frame.
+// ---------------------------------------------------------------------------
+constexpr int CLS_THREADS = 512;
+constexpr int CLS_PPT = ENC_TILE / CLS_THREADS;   // 2 pixels per thread
+constexpr int CLS_RING = 16384;                   // ring words (64 KB)
+// luma test offsets in Y space: R,B fields +16, G field +32, plus 256 per field
+constexpr uint32_t LUMA_KY = (256u + 16u) | ((256u + 32u) << 10) | ((256u + 16u) << 20);
+
+__device__ __forceinline__ uint32_t y_from_rgba(uint32_t v) {
+  const uint32_t s = spread_rgba(v);
+  const uint32_t g = (v >> 8) & 0xFFu;
+  return (s + K3(256u) - (g | (g << 20))) & K3(0xFFu);
+}
+__device__ __forceinline__ uint32_t rgb_from_y(uint32_t y) {
+  const uint32_t g = (y >> 10) & 0xFFu;
+  return (y + (g | (g << 20))) & K3(0xFFu);
+}
+
+struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W + px)
+  const uint32_t* ring;
+  uint32_t W;
+  int64_t i;
+  __device__ __forceinline__ uint32_t operator()(int rows, int px) const {
+    const int64_t j = i - ((int64_t)rows * W + px);
+    return rgb_from_y(ring[j & (CLS_RING - 1)]);
+  }
+};
+
+// Branch-free mode decision (every reference valid: i >= 3W+3, W >= 3) from
+// the Y ring; returns the record (same layout as classify_fast).
+__device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t i, uint32_t W) {
+  auto at = [&](uint32_t off) { return ring[(i - off) & (CLS_RING - 1)]; };
+  const uint32_t X = at(0), L = at(1), L2 = at(2), L3 = at(3);
+  const uint32_t U = at(W), UR1 = at(W - 1), UR3 = at(W - 3), UL3 = at(W + 3);
+  const uint32_t U2 = at(2 * W);
+  const uint32_t V = at(3 * W), VR1 = at(3 * W - 1), VL1 = at(3 * W + 1);
+  const uint32_t VL3 = at(3 * W + 3), VR3 = at(3 * W - 3);
+  // back references k = 1..4 (code.rs:191-206; Y equality == RGB equality)
+  const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  const bool br = e1 | e2 | e3 | e4;
+  const uint32_t bk = e1 ? 1u : e2 ? 2u : e3 ? 3u : 4u;
+  // prediction floor((U+L)/2) in RGB
+  const uint32_t xr = rgb_from_y(X);
+  const uint32_t pred = avg3(rgb_from_y(U), rgb_from_y(L));
+  // small diff (code.rs:208-247)
+  const uint32_t d = xr + K3(259u) - pred;
+  const bool sd = ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
+  const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
+  // luma2 against the prediction (code.rs:252-292)
+  const uint32_t pg = (pred >> 10) & 0xFFu;
+  const uint32_t py = (pred + K3(256u) - (pg | (pg << 20))) & K3(0xFFu);
+  const uint32_t xk = X + LUMA_KY;
+  const uint32_t t2 = xk - py;
+  const bool l2 = (t2 & LUMA_MASK) == 0;
+  // luma against 11 references, first hit wins (code.rs:293-339)
+  uint32_t lk = 11u, lt = 0u;
+  if (__any(!br && !sd && !l2)) {
+    const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
+#pragma unroll
+    for (int k = 10; k >= 0; --k) {
+      const uint32_t t = xk - refs[k];
+      const bool ok = (t & LUMA_MASK) == 0;
+      lk = ok ? (uint32_t)k : lk;
+      lt = ok ? t : lt;
+    }
+  }
+  const uint32_t r = xr + K3(256u) - pred;
+  const uint32_t rec_br = P_BACK_REF | (bk << 3);
+  const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
+  const uint32_t rec_l2 = P_LUMA2 | (((t2 >> 10) & 63u) << 3) | ((t2 & 31u) << 9) | (((t2 >> 20) & 31u) << 14);
+  const uint32_t rec_lu = P_LUMA | (lk << 3) | (((lt >> 10) & 63u) << 7) | ((lt & 31u) << 13) |
+                          (((lt >> 20) & 31u) << 18);
+  const uint32_t rec_rgb = P_RGB | ((r & 255u) << 3) | (((r >> 10) & 255u) << 11) | (((r >> 20) & 255u) << 19);
+  return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
+}
+
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
+  __shared__ uint32_t ring[CLS_RING];
+  __shared__ uint32_t hist[N_BINS];
+  __shared__ uint32_t mask[ENC_TILE / 32];
+  const uint32_t T = a.tiles_per_frame;
+  const uint64_t total_work = (uint64_t)a.n_frames * T;
+  const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
+  const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
+  if (w_begin >= w_end) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t W = a.W;
+  const int64_t N = (int64_t)W * a.H;
+  for (int b = tid; b < N_BINS; b += CLS_THREADS) hist[b] = 0;
+  // mode-prefix counts: modes 0..3 in 16-bit fields of pc, mode 4 in pc4
+  unsigned long long pc = 0;
+  uint32_t pc4 = 0;
+  auto flush = [&](uint32_t frame) {
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t v = (uint32_t)(pc >> (16 * m)) & 0xFFFFu;
+      if (v) atomicAdd(&hist[BIN_PREFIX + m], v);
+    }
+    if (pc4) atomicAdd(&hist[BIN_PREFIX + P_LUMA2], pc4);
+    pc = 0;
+    pc4 = 0;
+    __syncthreads();
+    for (int b = tid; b < N_BINS; b += CLS_THREADS) {
+      if (hist[b]) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], hist[b]);
+      hist[b] = 0;
+    }
+  };
+  // prefill: the 3 rows + 3 pixels before the first tile
+  uint32_t cur_frame = (uint32_t)(w_begin / T);
+  {
+    const int64_t start = (int64_t)(w_begin % T) * ENC_TILE;
+    const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
+    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)cur_frame * a.frame_stride);
+    for (int64_t j = lo + tid; j < start; j += CLS_THREADS) ring[j & (CLS_RING - 1)] = y_from_rgba(fr[j]);
+  }
+  // the first tile's pixels
+  uint32_t pf[CLS_PPT];
+  auto fetch = [&](uint64_t w, uint32_t (&v)[CLS_PPT]) {
+    const uint32_t f = (uint32_t)(w / T);
+    const int64_t start = (int64_t)(w % T) * ENC_TILE;
+    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int64_t j = start + q * CLS_THREADS + tid;
+      v[q] = j < N ? fr[j] : 0u;
+    }
+  };
+  fetch(w_begin, pf);
+  for (uint64_t w = w_begin; w < w_end; ++w) {
+    const uint32_t f = (uint32_t)(w / T);
+    const uint32_t tt = (uint32_t)(w % T);
+    if (f != cur_frame) { flush(cur_frame); cur_frame = f; }
+    const int64_t start = (int64_t)tt * ENC_TILE;
+    const int count = (int)min((int64_t)ENC_TILE, N - start);
+    // stage this tile (Y space), start loading the next
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int64_t j = start + q * CLS_THREADS + tid;
+      ring[j & (CLS_RING - 1)] = y_from_rgba(pf[q]);
+    }
+    if (w + 1 < w_end) fetch(w + 1, pf);
+    __syncthreads();
+    // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
+    uint32_t coded_bits = 0;
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const int64_t i = start + p;
+      const bool coded = p < count && (i == 0 || ring[i & (CLS_RING - 1)] != ring[(i - 1) & (CLS_RING - 1)]);
+      const unsigned long long bal = __ballot(coded);
+      if (lane == 0) {
+        const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
+        mask[wb] = (uint32_t)bal;
+        mask[wb + 1] = (uint32_t)(bal >> 32);
+      }
+      coded_bits |= (coded ? 1u : 0u) << q;
+    }
+    __syncthreads();
+    if (tid < 64) {   // first / last coded pixel of the tile: one wave, no loop
+      const uint32_t mw = tid < ENC_TILE / 32 ? mask[tid] : 0u;
+      const unsigned long long nz = __ballot(mw != 0);
+      if (tid == 0) {
+        const uint64_t t = (uint64_t)f * T + tt;
+        uint32_t first = NONE, last = NONE;
+        if (nz) {
+          const int fw = __builtin_ctzll(nz), lw = 63 - __builtin_clzll(nz);
+          first = (uint32_t)(start + fw * 32 + __builtin_ctz(mask[fw]));
+          last = (uint32_t)(start + lw * 32 + 31 - __builtin_clz(mask[lw]));
+        }
+        a.tile_first[t] = first;
+        a.tile_last[t] = last;
+      }
+    }
+    const bool fast = start >= 3 * (int64_t)W + 3;
+    uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      uint32_t rec = REC_UNCODED;
+      if (fast) {
+        const uint32_t rf = classify_ring(ring, (uint32_t)(start + p), W);
+        rec = coded ? rf : REC_UNCODED;
+      } else if (coded) {
+        PixSyms sy;
+        RingAcc acc{ring, W, start + p};
+        classify<false>((uint32_t)(start + p), W, acc, sy);
+        rec = rec_from_syms(sy);
+      }
+      if (p < count) recs[p] = rec;
+      if (coded) {
+        const uint32_t m = rec & 7u;
+        pc += m < 4u ? (1ull << (16u * m)) : 0ull;
+        pc4 += m == 4u ? 1u : 0u;
+        uint32_t b0, b1, b2, b3;
+        const uint32_t n = rec_bins(rec, b0, b1, b2, b3);
+        atomicAdd(&hist[b0], 1u);
+        if (n > 1) { atomicAdd(&hist[b1], 1u); atomicAdd(&hist[b2], 1u); }
+        if (n > 3) atomicAdd(&hist[b3], 1u);
+        const int nx = next_coded_local(mask, p);
+        if (nx < count && nx > p + 1) {
+          uint64_t mm = (uint64_t)(nx - p - 2);
+          while (true) {
+            atomicAdd(&hist[BIN_PREFIX + P_RUN1 + (uint32_t)(mm & 7u)], 1u);
+            if (mm < 8) break;
+            mm >>= 3;
+          }
+        }
+      }
+    }
+    // the mask is rewritten by the next tile only after its staging barrier
+  }
+  flush(cur_frame);
+}
+
+// ---------------------------------------------------------------------------
 // K2: runs crossing tile ends. One block (1024 threads) per frame.
 // tile_next[t] = first coded pixel after tile t (N if none).
 // ---------------------------------------------------------------------------
