@@ -25,7 +25,7 @@ from dataclasses import dataclass
 
 __all__ = [
     "Image", "encode", "decode", "encode_bytes", "decode_bytes", "encode_bound",
-    "encode_batch", "decode_batch", "Pipeline", "NiceError", "lib", "LIB_PATH",
+    "encode_batch", "decode_batch", "Context", "Pipeline", "NiceError", "lib", "LIB_PATH",
     "DEC_STRICT_REFERENCE", "DEC_ALPHA_FILL_FF", "DEC_TOLERANT_HEADER",
 ]
 
@@ -216,8 +216,13 @@ def _stream_ptr(torch, device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+class Context(_Ctx):
+    """A device context with its own scratch arena: calls on different torch
+    streams need different contexts to run concurrently."""
+
+
 def encode_batch(px, width: int, height: int, channels: int, out, out_len,
-                 channels_out: int | None = None, stream=None) -> None:
+                 channels_out: int | None = None, stream=None, ctx: "_Ctx | None" = None) -> None:
     """Encode ``px`` (uint8 cuda tensor [n_frames, W*H*channels]) into ``out``
     (uint8 cuda tensor [n_frames, stride >= encode_bound]); lengths into
     ``out_len`` (int64 cuda tensor [n_frames]).  Asynchronous on the current
@@ -227,14 +232,14 @@ def encode_batch(px, width: int, height: int, channels: int, out, out_len,
     n = px.shape[0]
     st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(torch, px.device)
     rc = lib().nice_encode_batch_dev(
-        _ctx(dev).ptr, st, ctypes.c_void_p(px.data_ptr()), px.stride(0), n, width, height,
+        (ctx or _ctx(dev)).ptr, st, ctypes.c_void_p(px.data_ptr()), px.stride(0), n, width, height,
         channels, channels if channels_out is None else channels_out,
         ctypes.c_void_p(out.data_ptr()), out.stride(0), ctypes.c_void_p(out_len.data_ptr()))
     _check(rc, "nice_encode_batch_dev")
 
 
 def decode_batch(streams, stream_len, width: int, height: int, out_channels: int, px, status,
-                 flags: int = DEC_ALPHA_FILL_FF, stream=None) -> None:
+                 flags: int = DEC_ALPHA_FILL_FF, stream=None, ctx: "_Ctx | None" = None) -> None:
     """Decode ``streams`` (uint8 cuda [n, stride]) with byte lengths ``stream_len``
     (int64 cuda [n]) into ``px`` (uint8 cuda [n, >= W*H*out_channels]); per-frame
     status codes into ``status`` (int32 cuda [n])."""
@@ -243,7 +248,7 @@ def decode_batch(streams, stream_len, width: int, height: int, out_channels: int
     n = streams.shape[0]
     st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(torch, streams.device)
     rc = lib().nice_decode_batch_dev(
-        _ctx(dev).ptr, st, ctypes.c_void_p(streams.data_ptr()), streams.stride(0),
+        (ctx or _ctx(dev)).ptr, st, ctypes.c_void_p(streams.data_ptr()), streams.stride(0),
         ctypes.c_void_p(stream_len.data_ptr()), n, width, height, out_channels,
         ctypes.c_void_p(px.data_ptr()), px.stride(0), flags, ctypes.c_void_p(status.data_ptr()))
     _check(rc, "nice_decode_batch_dev")

@@ -52,10 +52,10 @@ struct EncLayout {
   size_t zero_bytes, total;
   size_t o_hist, o_flags;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_thist;
 };
 
-EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
+EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist = true) {
   EncLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -78,6 +78,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   L.o_tbits = take((size_t)n_frames * T * 4);
   L.o_toff = take((size_t)n_frames * T * 8);
   L.o_dend = take((size_t)n_frames * 8);
+  L.o_thist = take(tile_hist ? (size_t)n_frames * T * TH_WORDS * 4 : 0);
   L.total = o;
   return L;
 }
@@ -236,6 +237,7 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.hdr_bitoff = base + L.o_hdrbitoff;
   a.recs = (uint32_t*)(base + L.o_recs);
   a.rec_stride = (N + 3) & ~3ull;
+  a.tile_hist = nullptr;   // set by the ring-classify path
   a.tile_bits = (uint32_t*)(base + L.o_tbits);
   a.tile_off = (unsigned long long*)(base + L.o_toff);
   a.data_end = (unsigned long long*)(base + L.o_dend);
@@ -267,7 +269,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   const uint32_t T = tiles_for(w, h);
-  EncLayout L = enc_layout(n_frames, T, N);
+  const bool ring = channels == 4 && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
+  EncLayout L = enc_layout(n_frames, T, N, ring);
   int rc = ctx->enc.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->enc.ptr;
@@ -284,7 +287,6 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     // flushes each block's LDS histogram once per frame
     // RGBA frames: ring-staged kernel (each pixel loaded once; >= 16 tiles per
     // block so the 3-row prefill is amortised, 2 blocks per CU)
-    const bool ring = channels == 4 && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
     uint64_t blocks = ring ? 512 : 2048;
     uint64_t per = (total_tiles + blocks - 1) / blocks;
     if (per < (ring ? 16u : 1u)) per = ring ? 16 : 1;
@@ -293,6 +295,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     a.tiles_per_block = (uint32_t)per;
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
+    if (ring) a.tile_hist = (uint32_t*)(base + L.o_thist);
     if (ring) hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
     else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     tm.end(st);
@@ -310,7 +313,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     // grid-stride over tiles: 8 blocks of 256 threads per CU (LDS ~21 KB each)
     const uint32_t tblocks = (uint32_t)(total_tiles < 2048 ? total_tiles : 2048);
     ctx->timer.begin(NICE_PH_ENC_TILEBITS, st);
-    hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
+    if (a.tile_hist) hipLaunchKernelGGL(enc_tilebits_hist, dim3(tblocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_TILESCAN, st);
     hipLaunchKernelGGL(enc_tilescan, dim3(n_frames), dim3(1024), 0, st, a);
@@ -631,7 +635,7 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (channels == 4 && ((uintptr_t)d_px & 3)) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
-  EncLayout L = enc_layout(1, T, band_px1 - band_px0);
+  EncLayout L = enc_layout(1, T, band_px1 - band_px0, false);
   int rc = ctx->band.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->band.ptr;

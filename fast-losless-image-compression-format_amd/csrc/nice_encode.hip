@@ -424,7 +424,8 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
 
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   __shared__ uint32_t ring[CLS_RING];
-  __shared__ uint32_t hist[N_BINS];
+  __shared__ uint32_t hist[N_BINS + 64];   // + a discard slot per lane (absent symbols)
+  __shared__ uint32_t snap[N_BINS];        // hist after the previous tile
   __shared__ uint32_t mask[ENC_TILE / 32];
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total_work = (uint64_t)a.n_frames * T;
@@ -434,24 +435,13 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t W = a.W;
   const int64_t N = (int64_t)W * a.H;
-  for (int b = tid; b < N_BINS; b += CLS_THREADS) hist[b] = 0;
-  // mode-prefix counts: modes 0..3 in 16-bit fields of pc, mode 4 in pc4
-  unsigned long long pc = 0;
-  uint32_t pc4 = 0;
+  for (int b = tid; b < N_BINS; b += CLS_THREADS) { hist[b] = 0; snap[b] = 0; }
   auto flush = [&](uint32_t frame) {
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const uint32_t v = (uint32_t)(pc >> (16 * m)) & 0xFFFFu;
-      if (v) atomicAdd(&hist[BIN_PREFIX + m], v);
-    }
-    if (pc4) atomicAdd(&hist[BIN_PREFIX + P_LUMA2], pc4);
-    pc = 0;
-    pc4 = 0;
     __syncthreads();
     for (int b = tid; b < N_BINS; b += CLS_THREADS) {
       if (hist[b]) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], hist[b]);
       hist[b] = 0;
+      snap[b] = 0;
     }
   };
   // prefill: the 3 rows + 3 pixels before the first tile
@@ -491,12 +481,14 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     __syncthreads();
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
+    unsigned long long wbal[CLS_PPT];   // coded flags of the wave's 64 pixels per q
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
       const int p = q * CLS_THREADS + tid;
       const int64_t i = start + p;
       const bool coded = p < count && (i == 0 || ring[i & (CLS_RING - 1)] != ring[(i - 1) & (CLS_RING - 1)]);
       const unsigned long long bal = __ballot(coded);
+      wbal[q] = bal;
       if (lane == 0) {
         const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
         mask[wb] = (uint32_t)bal;
@@ -537,16 +529,22 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
         rec = rec_from_syms(sy);
       }
       if (p < count) recs[p] = rec;
-      if (coded) {
-        const uint32_t m = rec & 7u;
-        pc += m < 4u ? (1ull << (16u * m)) : 0ull;
-        pc4 += m == 4u ? 1u : 0u;
+      {
+        // prefix and payload symbols: five unconditional LDS adds, absent ones
+        // into this lane's discard slot (no divergent branches)
         uint32_t b0, b1, b2, b3;
         const uint32_t n = rec_bins(rec, b0, b1, b2, b3);
-        atomicAdd(&hist[b0], 1u);
-        if (n > 1) { atomicAdd(&hist[b1], 1u); atomicAdd(&hist[b2], 1u); }
-        if (n > 3) atomicAdd(&hist[b3], 1u);
-        const int nx = next_coded_local(mask, p);
+        const uint32_t dump = N_BINS + (uint32_t)lane;
+        atomicAdd(&hist[coded ? BIN_PREFIX + (rec & 7u) : dump], 1u);
+        atomicAdd(&hist[coded ? b0 : dump], 1u);
+        atomicAdd(&hist[coded && n > 1 ? b1 : dump], 1u);
+        atomicAdd(&hist[coded && n > 1 ? b2 : dump], 1u);
+        atomicAdd(&hist[coded && n > 3 ? b3 : dump], 1u);
+      }
+      if (coded) {
+        // next coded pixel: in this wave's 64 pixels from the ballot, else the tile mask
+        const unsigned long long above = lane < 63 ? (wbal[q] >> (lane + 1)) : 0ull;
+        const int nx = above ? p + 1 + (int)__builtin_ctzll(above) : next_coded_local(mask, p | 63);
         if (nx < count && nx > p + 1) {
           uint64_t mm = (uint64_t)(nx - p - 2);
           while (true) {
@@ -557,7 +555,20 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
         }
       }
     }
-    // the mask is rewritten by the next tile only after its staging barrier
+    // this tile's symbol counts (histogram growth since the previous tile),
+    // for enc_tilebits_hist: 858 u16 counts as u32 pairs
+    __syncthreads();
+    if (tid < (int)TH_WORDS) {
+      uint32_t wv = 0;
+      if (2 * tid < N_BINS) {
+        const int b = 2 * tid;
+        const uint32_t h0 = hist[b], h1 = hist[b + 1];
+        wv = ((h0 - snap[b]) & 0xFFFFu) | ((h1 - snap[b + 1]) << 16);
+        snap[b] = h0;
+        snap[b + 1] = h1;
+      }
+      a.tile_hist[((uint64_t)f * T + tt) * TH_WORDS + tid] = wv;
+    }
   }
   flush(cur_frame);
 }
@@ -962,6 +973,57 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
     if (lane == 0) wsum[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) a.tile_bits[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  }
+}
+
+// Tile bits from the per-tile symbol counts of enc_classify_ring: sum of
+// count x code length over the 858 bins, plus the run digits of the tile's
+// last run (it ends at tile_next, in a later tile; code.rs:371-407).
+__global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
+  __shared__ uint32_t lens[2 * TH_WORDS];
+  __shared__ uint32_t wsum[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t T = a.tiles_per_frame;
+  uint32_t cur_f = 0xFFFFFFFFu;
+  uint64_t t0, t1;
+  tile_range(a, t0, t1);
+  for (uint64_t w = t0; w < t1; ++w) {
+    const uint64_t t = work_tile(a, w);
+    const uint32_t f = (uint32_t)(t / T);
+    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
+    if (f != cur_f) {
+      __syncthreads();
+      for (int b = threadIdx.x; b < (int)(2 * TH_WORDS); b += 256)
+        lens[b] = b < N_BINS ? (a.tbl[(uint64_t)f * N_BINS + b] & 31u) : 0u;
+      cur_f = f;
+      __syncthreads();
+    }
+    const uint32_t* th = a.tile_hist + t * TH_WORDS;
+    uint32_t acc = 0;
+    for (int k = threadIdx.x; k < (int)TH_WORDS; k += 256) {
+      const uint32_t v = th[k];
+      acc += (v & 0xFFFFu) * lens[2 * k] + (v >> 16) * lens[2 * k + 1];
+    }
+    if (threadIdx.x == 0) {
+      const uint32_t last = a.tile_last[t];
+      if (last != NONE) {
+        const uint64_t run = (uint64_t)a.tile_next[t] - last - 1;
+        if (run > 0) {
+          uint64_t m = run - 1;
+          while (true) {
+            acc += lens[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
+            if (m < 8) break;
+            m >>= 3;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    __syncthreads();
+    if (lane == 0) wsum[wid] = acc;
     __syncthreads();
     if (threadIdx.x == 0) a.tile_bits[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   }

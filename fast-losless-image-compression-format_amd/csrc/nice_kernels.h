@@ -37,6 +37,7 @@ struct EncArgs {
   uint8_t* hdr_bitoff;       // n_frames
   uint32_t* recs;            // n_frames * rec_stride per-pixel symbol records
   uint64_t rec_stride;       // W*H rounded up to 4
+  uint32_t* tile_hist;       // n_frames * T * TH_WORDS: per-tile symbol counts, u16 pairs (ring path), else null
   uint32_t* tile_bits;       // n_frames * T: data bits per tile
   unsigned long long* tile_off;   // n_frames * T: absolute bit offset of each tile
   unsigned long long* data_end;   // n_frames: bit position after the last data bit
@@ -60,6 +61,8 @@ __global__ void enc_tailruns(EncArgs a);
 __global__ void enc_tables(EncArgs a);
 __global__ void enc_header(EncArgs a);
 __global__ void enc_tilebits(EncArgs a);
+__global__ void enc_tilebits_hist(EncArgs a);
+constexpr uint32_t TH_WORDS = 432;   // u32 words per tile histogram (858 u16 counts, 16-B aligned rows)
 __global__ void enc_tilescan(EncArgs a);
 __global__ void enc_pack(EncArgs a);
 __global__ void enc_tail(EncArgs a);
