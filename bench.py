@@ -109,17 +109,27 @@ def max_over_ranks(value, dist, device):
     return float(t.item())
 
 
-def load_traffic(kernel, frames, path=None):
-    """Per-launch HBM bytes of `kernel` from the committed PMC summary (bytes per
-    frame from separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected; see
-    profiles/README.md), scaled to this launch's frame count; None if absent."""
-    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
+# timing phase -> the kernels that implement it (first match in the PMC summary)
+PHASE_KERNELS = {"enc_classify": ["enc_classify_ring", "enc_classify"],
+                 "enc_tilebits": ["enc_tilebits_hist", "enc_tilebits"],
+                 "dec_reconstruct": ["dec_rows", "dec_rows_wide", "dec_reconstruct"]}
+
+
+def load_traffic(phase, frames, path=None):
+    """Per-launch HBM bytes of the kernel behind `phase` from the committed PMC
+    summary (bytes per frame from separate FETCH_SIZE / WRITE_SIZE passes,
+    gfx950-corrected; see profiles/README.md), scaled to this launch's frame
+    count; None if absent."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r01d.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return int(d["kernels"][kernel]["hbm_bytes_per_frame"] * frames)
-    except (OSError, KeyError, ValueError):
+    except (OSError, ValueError):
         return None
+    for k in PHASE_KERNELS.get(phase, [phase]):
+        if k in d.get("kernels", {}):
+            return int(d["kernels"][k]["hbm_bytes_per_frame"] * frames)
+    return None
 
 
 def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):

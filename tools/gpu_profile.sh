@@ -3,7 +3,7 @@
 # Usage (from the repo root on the GPU box): bash tools/gpu_profile.sh TAG [FRAMES]
 set -e
 TAG=${1:-r01}
-FR=${2:-256}
+FR=${2:-512}
 R=$(pwd)
 O=$R/gpurun_out/$TAG
 S=/tmp/prof_$TAG
@@ -15,11 +15,11 @@ timeout -k 10 400 python bench.py --frames $FR > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $S/kt -o run -- \
-  python3 $R/bench.py --frames $FR --steps 3 --warmup 1 --no-cpu-baseline > $O/kt.log 2>&1
+  python3 $R/bench.py --frames $FR --steps 3 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/kt.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $S/pmc_fetch -o run -- \
-  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1
+  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $S/pmc_write -o run -- \
-  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1
+  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_write.log 2>&1
 cd $R
 find $S -name "*.csv" -exec ls -la {} \; > $O/files.txt
 cp $(find $S/kt -name "*kernel_stats.csv") $O/kernel_stats.csv
