@@ -150,6 +150,12 @@ int nice_pipe_encode(nice_pipe* p, const uint8_t* const* px, uint32_t n_frames, 
 int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, const uint64_t* stream_len, uint32_t n_frames,
                      uint8_t out_channels, uint8_t* const* px, uint32_t flags, int32_t* status);
 
+/* ---- command-line front end helper (host only) ----
+ * Reverses the PNG scanline filters (types 0-4) of h rows of w pixels of bpp
+ * bytes: raw = h x (1 filter byte + w*bpp bytes), out = h x w*bpp bytes.  The
+ * reference CLI (main.rs:28-133) reads and writes PNG with the png crate. */
+int nice_png_unfilter(const uint8_t* raw, uint32_t w, uint32_t h, uint32_t bpp, uint8_t* out);
+
 /* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
 enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,
