@@ -492,9 +492,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // single-wave kernel otherwise
   const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
-  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * w) * 4;
+  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 1)) * 4;
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
-  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * w * 4)
+  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 1) * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
   DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf);
   int rc = ctx->dec.grow(L.total);

@@ -1119,6 +1119,8 @@ __device__ __forceinline__ void rows_barrier() {
   }
 }
 
+__host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 1; }
+
 template <int MAXT, bool LDS_RING>
 __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   constexpr int S = ROWS_SEG;
@@ -1131,7 +1133,10 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   uint32_t* pend = head3 + 4;           // 2 round flags
   int* err = reinterpret_cast<int*>(pend + 2);
   const uint32_t f = blockIdx.x;
-  uint32_t* ring = LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * W);
+  // ring rows padded one word per 16 pixels: lane i's segment starts at bank
+  // 17i mod 32, so the lanes' accesses to their segments are conflict free
+  const uint32_t RS = rows_ring_stride(W);
+  uint32_t* ring = LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * RS);
   if (a.status[f] != 0) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t nseg = (W + S - 1) / S;
@@ -1182,7 +1187,8 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const bool up = cls >= 4;
       const bool cur = up && back == 0;
       // unconditional LDS read (a harmless in-range address for other classes)
-      const uint32_t o = ring[(size_t)((y - back) & (ROWS_RING - 1)) * W + (uint32_t)min(max(tx, 0), (int)W - 1)];
+      const uint32_t txc = (uint32_t)min(max(tx, 0), (int)W - 1);
+      const uint32_t o = ring[(size_t)((y - back) & (ROWS_RING - 1)) * RS + txc + (txc >> 4)];
       const uint32_t c = spread3(r & 0xFFFFFFu);
       const uint32_t kb = cls == 0 ? (y == 0 ? W_L1 : W_AVG)
                         : cls < 4 ? (W_L1 << (cls - 1u)) : (cur ? W_CUR : 0u);
@@ -1194,10 +1200,10 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       if (y == 0) {
         r0 = r1 = r2 = ivs_exact(0u);
       } else {
-        const uint32_t* pr = ring + (size_t)((y - 1) & (ROWS_RING - 1)) * W;
-        r0 = ivs_exact(pr[W - 1]);
-        r1 = ivs_exact(pr[W - 2]);
-        r2 = ivs_exact(pr[W - 3]);
+        const uint32_t* pr = ring + (size_t)((y - 1) & (ROWS_RING - 1)) * RS;
+        r0 = ivs_exact(pr[(W - 1) + ((W - 1) >> 4)]);
+        r1 = ivs_exact(pr[(W - 2) + ((W - 2) >> 4)]);
+        r2 = ivs_exact(pr[(W - 3) + ((W - 3) >> 4)]);
       }
     }
     if (y + 1 < H) load_recs(y + 1);   // in flight during this row
@@ -1263,7 +1269,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     const unsigned long long c3 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- emit: ring row y (its slot held row y-4, no longer referenced) and the raster
     if (active) {
-      uint32_t* rr = ring + (size_t)(y & (ROWS_RING - 1)) * W + x0;
+      uint32_t* rr = ring + (size_t)(y & (ROWS_RING - 1)) * RS + x0 + (x0 >> 4);   // x0 = 16 * lane
       const uint64_t pix = (uint64_t)y * W + x0;
 #pragma unroll
       for (int p = 0; p < S; ++p)

@@ -1,0 +1,37 @@
+"""Diagnostic: decode time per phase for N device-generated 4K frames."""
+import ctypes, importlib, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import bench
+nice = importlib.import_module("fast-losless-image-compression-format_amd")
+W, H, n = 3840, 2160, int(os.environ.get("NF", 128))
+dev = torch.device("cuda", 0)
+px = bench.syn_frames(torch, n, W, H, 1, dev)
+bound = (nice.encode_bound(W, H) + 255) // 256 * 256
+out = torch.zeros((n, bound), dtype=torch.uint8, device=dev)
+lens = torch.zeros(n, dtype=torch.int64, device=dev)
+nice.encode_batch(px, W, H, 4, out, lens)
+dec = torch.empty((n, W * H * 4), dtype=torch.uint8, device=dev)
+st = torch.zeros(n, dtype=torch.int32, device=dev)
+L = nice.lib()
+L.nice_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.nice_ctx_read_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+L.nice_phase_name.restype = ctypes.c_char_p
+nice.decode_batch(out, lens, W, H, 4, dec, st)
+torch.cuda.synchronize()
+ok = int(st.abs().sum()) == 0 and torch.equal(dec.view(n, -1, 4)[:, :, :3], px.view(n, -1, 4)[:, :, :3])
+ctx = nice._ctx(0)
+L.nice_ctx_set_timing(ctx.ptr, 1)
+t0 = time.perf_counter()
+for _ in range(3):
+    nice.decode_batch(out, lens, W, H, 4, dec, st)
+torch.cuda.synchronize()
+el = (time.perf_counter() - t0) / 3
+ms = (ctypes.c_double * 32)(); cnt = (ctypes.c_uint32 * 32)()
+L.nice_ctx_read_timing(ctx.ptr, ms, cnt)
+ph = {L.nice_phase_name(i).decode(): round(ms[i] / 3, 2) for i in range(32) if cnt[i]}
+print(f"decode {n} x 4K: {el*1e3:.2f} ms ok={ok} {ph}", flush=True)
+one = (out[:1], lens[:1], dec[:1], st[:1])
+nice.decode_batch(one[0], one[1], W, H, 4, one[2], one[3]); torch.cuda.synchronize()
+t0 = time.perf_counter(); nice.decode_batch(one[0], one[1], W, H, 4, one[2], one[3]); torch.cuda.synchronize()
+print(f"decode 1 x 4K: {(time.perf_counter()-t0)*1e3:.2f} ms", flush=True)
