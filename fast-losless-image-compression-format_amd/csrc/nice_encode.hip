@@ -141,20 +141,43 @@ __device__ __forceinline__ uint32_t rec_from_syms(const PixSyms& s) {
   }
 }
 
-// Payload bins of a coded record (n = 1, 3 or 4), branch-free.
+// Payload bins of a coded record (n = 1, 3 or 4), branch-free: per mode m
+// (record bits 0..2), payload k is bits [shift, shift+width) of the record plus
+// a histogram base, all looked up in packed constants (no per-mode control flow).
+//   m:        0 BACK_REF   1 RGB        2 LUMA        3 SMALL_DIFF  4 LUMA2
+//   k = 0     847+[3,3)    0+[3,8)      365+[3,4)     376+[3,9)     719+[3,6)
+//   k = 1     -            0+[11,8)     269+[7,6)     -             783+[9,5)
+//   k = 2     -            0+[19,8)     333+[13,5)    -             815+[14,5)
+//   k = 3     -            -            333+[18,5)    -             -
+constexpr unsigned long long rb_pack(int a0, int a1, int a2, int a3, int a4, int bits) {
+  return (unsigned long long)a0 | ((unsigned long long)a1 << bits) | ((unsigned long long)a2 << (2 * bits)) |
+         ((unsigned long long)a3 << (3 * bits)) | ((unsigned long long)a4 << (4 * bits));
+}
+// base (10 bits per mode), shift (5) | width << 5 (10 bits per mode)
+constexpr unsigned long long RB_BASE[4] = {
+    rb_pack(BIN_BACK_REF, 0, BIN_LUMA_REF, BIN_SMALL_DIFF, BIN_LUMA2_BASE, 10),
+    rb_pack(0, 0, BIN_LUMA_BASE, 0, BIN_LUMA2_R, 10),
+    rb_pack(0, 0, BIN_LUMA_OTHER, 0, BIN_LUMA2_B, 10),
+    rb_pack(0, 0, BIN_LUMA_OTHER, 0, 0, 10)};
+constexpr unsigned long long RB_FIELD[4] = {
+    rb_pack(3 | 3 << 5, 3 | 8 << 5, 3 | 4 << 5, 3 | 9 << 5, 3 | 6 << 5, 10),
+    rb_pack(0, 11 | 8 << 5, 7 | 6 << 5, 0, 9 | 5 << 5, 10),
+    rb_pack(0, 19 | 8 << 5, 13 | 5 << 5, 0, 14 | 5 << 5, 10),
+    rb_pack(0, 0, 18 | 5 << 5, 0, 0, 10)};
+constexpr uint32_t RB_N = 1u | 3u << 3 | 4u << 6 | 1u << 9 | 3u << 12;   // payload count, 3 bits per mode
+__device__ __forceinline__ uint32_t rb_bin(uint32_t rec, uint32_t m, int k) {
+  const uint32_t base = (uint32_t)(RB_BASE[k] >> (10u * m)) & 0x3FFu;
+  const uint32_t fw = (uint32_t)(RB_FIELD[k] >> (10u * m)) & 0x3FFu;
+  return base + __builtin_amdgcn_ubfe(rec, fw & 31u, fw >> 5);
+}
 __device__ __forceinline__ uint32_t rec_bins(uint32_t rec, uint32_t& b0, uint32_t& b1, uint32_t& b2,
                                              uint32_t& b3) {
-  const uint32_t m = rec & 7u;
-  const uint32_t x = rec >> 3;
-  const bool br = m == P_BACK_REF, sd = m == P_SMALL_DIFF, l2 = m == P_LUMA2, lu = m == P_LUMA;
-  b0 = br ? BIN_BACK_REF + (x & 7u)
-     : sd ? BIN_SMALL_DIFF + (x & 511u)
-     : l2 ? BIN_LUMA2_BASE + (x & 63u)
-     : lu ? BIN_LUMA_REF + (x & 15u) : (x & 255u);
-  b1 = l2 ? BIN_LUMA2_R + ((x >> 6) & 31u) : lu ? BIN_LUMA_BASE + ((x >> 4) & 63u) : ((x >> 8) & 255u);
-  b2 = l2 ? BIN_LUMA2_B + ((x >> 11) & 31u) : lu ? BIN_LUMA_OTHER + ((x >> 10) & 31u) : ((x >> 16) & 255u);
-  b3 = BIN_LUMA_OTHER + ((x >> 15) & 31u);
-  return (br || sd) ? 1u : lu ? 4u : 3u;
+  const uint32_t m = min(rec & 7u, 4u);
+  b0 = rb_bin(rec, m, 0);
+  b1 = rb_bin(rec, m, 1);
+  b2 = rb_bin(rec, m, 2);
+  b3 = rb_bin(rec, m, 3);
+  return (RB_N >> (3u * m)) & 7u;
 }
 
 // Branch-free mode decision for a pixel whose every reference exists
