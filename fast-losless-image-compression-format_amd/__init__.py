@@ -30,7 +30,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnice_hip.so")
+# NICE_LIB_PATH: an alternative build of the same library (tools/ A/B timing)
+LIB_PATH = os.environ.get("NICE_LIB_PATH") or os.path.join(_HERE, "libnice_hip.so")
 
 OK, E_ARG, E_HIP, E_NODEV, E_CAPACITY, E_FORMAT, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 _ERRNAMES = {E_ARG: "bad argument", E_HIP: "HIP runtime failure", E_NODEV: "no gfx950 device",

@@ -179,6 +179,33 @@ __device__ __forceinline__ uint32_t rec_bins(uint32_t rec, uint32_t& b0, uint32_
   b3 = rb_bin(rec, m, 3);
   return (RB_N >> (3u * m)) & 7u;
 }
+// The same from an LDS table (one 16-byte read per record): row m (record
+// bits 0..2; rows 5..7 empty), word k = base | shift << 10 | width << 15, the
+// payload count in bits 20..22 of word 0.
+struct RecBinTable { uint4 row[8]; };
+__device__ __forceinline__ void rbt_init(RecBinTable& t, int tid) {
+  if (tid < 8) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t m = (uint32_t)tid;
+      const uint32_t base = m < 5 ? (uint32_t)(RB_BASE[k] >> (10u * m)) & 0x3FFu : 0u;
+      const uint32_t fw = m < 5 ? (uint32_t)(RB_FIELD[k] >> (10u * m)) & 0x3FFu : 0u;
+      w[k] = base | (fw & 31u) << 10 | (fw >> 5) << 15;
+    }
+    w[0] |= (tid < 5 ? (RB_N >> (3u * tid)) & 7u : 0u) << 20;
+    t.row[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+__device__ __forceinline__ uint32_t rec_bins(const RecBinTable& t, uint32_t rec, uint32_t& b0, uint32_t& b1,
+                                             uint32_t& b2, uint32_t& b3) {
+  const uint4 r = t.row[rec & 7u];
+  b0 = (r.x & 0x3FFu) + __builtin_amdgcn_ubfe(rec, (r.x >> 10) & 31u, (r.x >> 15) & 31u);
+  b1 = (r.y & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.y >> 10, r.y >> 15);
+  b2 = (r.z & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.z >> 10, r.z >> 15);
+  b3 = (r.w & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.w >> 10, r.w >> 15);
+  return r.x >> 20;
+}
 
 // Branch-free mode decision for a pixel whose every reference exists
 // (i >= 3W+3, W >= 3): all tests are evaluated and the first hit in the
@@ -374,6 +401,10 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
 constexpr int CLS_THREADS = 512;
 constexpr int CLS_PPT = ENC_TILE / CLS_THREADS;   // 2 pixels per thread
 constexpr int CLS_RING = 16384;                   // ring words (64 KB)
+// words 0..7 of the ring mirrored past its end: a neighbour group (pixels
+// b .. b+6 for b = (i - rows*W - 3) mod CLS_RING) is one base address plus
+// immediate offsets, never wrapping
+constexpr int CLS_GUARD = 8;
 // luma test offsets in Y space: R,B fields +16, G field +32, plus 256 per field
 constexpr uint32_t LUMA_KY = (256u + 16u) | ((256u + 32u) << 10) | ((256u + 16u) << 20);
 
@@ -398,14 +429,18 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 };
 
 // Branch-free mode decision (every reference valid: i >= 3W+3, W >= 3) from
-// the Y ring; returns the record (same layout as classify_fast).
+// the Y ring; returns the record (same layout as classify_fast).  Four base
+// addresses (rows 0..3 back, 3 pixels left), the rest immediate offsets.
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t i, uint32_t W) {
-  auto at = [&](uint32_t off) { return ring[(i - off) & (CLS_RING - 1)]; };
-  const uint32_t X = at(0), L = at(1), L2 = at(2), L3 = at(3);
-  const uint32_t U = at(W), UR1 = at(W - 1), UR3 = at(W - 3), UL3 = at(W + 3);
-  const uint32_t U2 = at(2 * W);
-  const uint32_t V = at(3 * W), VR1 = at(3 * W - 1), VL1 = at(3 * W + 1);
-  const uint32_t VL3 = at(3 * W + 3), VR3 = at(3 * W - 3);
+  const uint32_t* b0 = ring + ((i - 3u) & (CLS_RING - 1));
+  const uint32_t* b1 = ring + ((i - W - 3u) & (CLS_RING - 1));
+  const uint32_t* b2 = ring + ((i - 2u * W) & (CLS_RING - 1));
+  const uint32_t* b3 = ring + ((i - 3u * W - 3u) & (CLS_RING - 1));
+  const uint32_t X = b0[3], L = b0[2], L2 = b0[1], L3 = b0[0];
+  const uint32_t U = b1[3], UR1 = b1[4], UR3 = b1[6], UL3 = b1[0];
+  const uint32_t U2 = b2[0];
+  const uint32_t V = b3[3], VR1 = b3[4], VL1 = b3[2];
+  const uint32_t VL3 = b3[0], VR3 = b3[6];
   // back references k = 1..4 (code.rs:191-206; Y equality == RGB equality)
   const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
   const bool br = e1 | e2 | e3 | e4;
@@ -446,16 +481,18 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
 }
 
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
-  __shared__ uint32_t ring[CLS_RING];
+  __shared__ uint32_t ring[CLS_RING + CLS_GUARD];
   __shared__ uint32_t hist[N_BINS + 64];   // + a discard slot per lane (absent symbols)
   __shared__ uint32_t snap[N_BINS];        // hist after the previous tile
   __shared__ uint32_t mask[ENC_TILE / 32];
+  __shared__ RecBinTable rbt;
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total_work = (uint64_t)a.n_frames * T;
   const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
   const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
   if (w_begin >= w_end) return;
   const int tid = threadIdx.x, lane = tid & 63;
+  rbt_init(rbt, tid);
   const uint32_t W = a.W;
   const int64_t N = (int64_t)W * a.H;
   for (int b = tid; b < N_BINS; b += CLS_THREADS) { hist[b] = 0; snap[b] = 0; }
@@ -473,7 +510,11 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     const int64_t start = (int64_t)(w_begin % T) * ENC_TILE;
     const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
     const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)cur_frame * a.frame_stride);
-    for (int64_t j = lo + tid; j < start; j += CLS_THREADS) ring[j & (CLS_RING - 1)] = y_from_rgba(fr[j]);
+    for (int64_t j = lo + tid; j < start; j += CLS_THREADS) {
+      const uint32_t k = (uint32_t)j & (CLS_RING - 1), y = y_from_rgba(fr[j]);
+      ring[k] = y;
+      if (k < CLS_GUARD) ring[CLS_RING + k] = y;
+    }
   }
   // the first tile's pixels
   uint32_t pf[CLS_PPT];
@@ -497,8 +538,9 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     // stage this tile (Y space), start loading the next
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
-      const int64_t j = start + q * CLS_THREADS + tid;
-      ring[j & (CLS_RING - 1)] = y_from_rgba(pf[q]);
+      const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (CLS_RING - 1), y = y_from_rgba(pf[q]);
+      ring[k] = y;
+      if (k < CLS_GUARD) ring[CLS_RING + k] = y;
     }
     if (w + 1 < w_end) fetch(w + 1, pf);
     __syncthreads();
@@ -509,7 +551,8 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     for (int q = 0; q < CLS_PPT; ++q) {
       const int p = q * CLS_THREADS + tid;
       const int64_t i = start + p;
-      const bool coded = p < count && (i == 0 || ring[i & (CLS_RING - 1)] != ring[(i - 1) & (CLS_RING - 1)]);
+      const uint32_t* bl = ring + ((uint32_t)(i - 1) & (CLS_RING - 1));
+      const bool coded = p < count && (i == 0 || bl[1] != bl[0]);
       const unsigned long long bal = __ballot(coded);
       wbal[q] = bal;
       if (lane == 0) {
@@ -553,12 +596,22 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       }
       if (p < count) recs[p] = rec;
       {
-        // prefix and payload symbols: five unconditional LDS adds, absent ones
-        // into this lane's discard slot (no divergent branches)
+        // prefix counts per wave (ballots; lanes 0..4 add them), payload
+        // symbols: four unconditional LDS adds, absent ones into this lane's
+        // discard slot (no divergent branches)
         uint32_t b0, b1, b2, b3;
-        const uint32_t n = rec_bins(rec, b0, b1, b2, b3);
+        const uint32_t n = rec_bins(rbt, rec, b0, b1, b2, b3);
         const uint32_t dump = N_BINS + (uint32_t)lane;
-        atomicAdd(&hist[coded ? BIN_PREFIX + (rec & 7u) : dump], 1u);
+        {
+          const uint32_t m = rec & 7u;   // REC_UNCODED (7) for run members
+          uint32_t pc = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < 5; ++k) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(m == k));
+            pc = (uint32_t)lane == k ? c : pc;
+          }
+          if (lane < 5 && pc) atomicAdd(&hist[BIN_PREFIX + lane], pc);
+        }
         atomicAdd(&hist[coded ? b0 : dump], 1u);
         atomicAdd(&hist[coded && n > 1 ? b1 : dump], 1u);
         atomicAdd(&hist[coded && n > 1 ? b2 : dump], 1u);
@@ -915,8 +968,8 @@ __device__ __forceinline__ void quad_mask(const uint32_t (&rc)[4], int lane, int
 
 // Runs, code entries and bit counts -- phase 2 (after the mask barrier).
 // Branch-free apart from the run digits: absent symbols get entry 0 (length 0).
-__device__ __forceinline__ void quad_bits(const uint32_t* tbl, const uint32_t* mask, int64_t start, int count,
-                                          int p0, uint32_t next_tile_px, TileQuad& Q) {
+__device__ __forceinline__ void quad_bits(const uint32_t* tbl, const RecBinTable& rbt, const uint32_t* mask,
+                                          int64_t start, int count, int p0, uint32_t next_tile_px, TileQuad& Q) {
   const int nx_local = next_coded_local(mask, p0 + 3);
   const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)next_tile_px;
   Q.nb = 0;
@@ -924,7 +977,7 @@ __device__ __forceinline__ void quad_bits(const uint32_t* tbl, const uint32_t* m
   for (int q = 0; q < 4; ++q) {
     const bool coded = (Q.nib >> q) & 1u;
     uint32_t b0, b1, b2, b3;
-    const uint32_t n = rec_bins(Q.rc[q], b0, b1, b2, b3);
+    const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
     const uint32_t t0 = tbl[BIN_PREFIX + min(Q.rc[q] & 7u, 4u)], t1 = tbl[b0], t2 = tbl[b1], t3 = tbl[b2],
                    t4 = tbl[b3];
     Q.e[q][0] = coded ? t0 : 0u;
@@ -969,6 +1022,8 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
+  __shared__ RecBinTable rbt;
+  rbt_init(rbt, threadIdx.x);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t T = a.tiles_per_frame;
   const int64_t N = (int64_t)a.W * a.H;
@@ -991,7 +1046,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
     TileQuad Q;
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
-    quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
+    quad_bits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
     uint32_t x = Q.nb;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
@@ -1095,6 +1150,8 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
+  __shared__ RecBinTable rbt;
+  rbt_init(rbt, threadIdx.x);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total = (uint64_t)a.n_frames * T;
@@ -1121,7 +1178,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
     TileQuad Q;
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
-    quad_bits(tbl, mask, start, count, p0, a.tile_next[t], Q);
+    quad_bits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
     uint32_t x = Q.nb;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y2 = __shfl_up(x, o);
@@ -1151,13 +1208,39 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
           ++wi;
         }
       };
+      // n <= 32 bits of val (0 when n == 0)
+      auto put_n = [&](uint32_t val, uint32_t n) {
+        acc |= (uint64_t)val << ((64u - nacc - n) & 63u);
+        nacc += n;
+        if (nacc >= 32u) {
+          atomicOr(&bits[wi], (uint32_t)(acc >> 32));
+          acc <<= 32;
+          nacc -= 32u;
+          ++wi;
+        }
+      };
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        put(Q.e[q][0]);
-        put(Q.e[q][1]);
-        put(Q.e[q][2]);
-        put(Q.e[q][3]);
-        put(Q.e[q][4]);
+        // the pixel's codes as one value (two puts) when they fit 64 bits
+        uint64_t v = 0;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const uint32_t e = Q.e[q][k], n = e & 31u;
+          v = (v << n) | (e >> 5);
+          tot += n;
+        }
+        if (tot <= 64u) {
+          const bool two = tot > 32u;
+          put_n(two ? (uint32_t)(v >> 32) : 0u, two ? tot - 32u : 0u);
+          put_n((uint32_t)v, two ? 32u : tot);
+        } else {
+          put(Q.e[q][0]);
+          put(Q.e[q][1]);
+          put(Q.e[q][2]);
+          put(Q.e[q][3]);
+          put(Q.e[q][4]);
+        }
         if (Q.run[q] > 0) {
           uint64_t m = Q.run[q] - 1;
           while (true) {

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 counter CSVs per kernel (last dispatch of each kernel)."""
+"""Summarise rocprofv3 counter CSVs per kernel (the longest dispatch of each kernel)."""
 import csv, collections, glob, sys
 for path in sys.argv[1:]:
     rows = list(csv.DictReader(open(path)))
@@ -10,7 +10,8 @@ for path in sys.argv[1:]:
         d["_dur_us"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     last = {}
     for (k, _), d in agg.items():
-        last[k] = d
+        if k not in last or d["_dur_us"] >= last[k]["_dur_us"]:
+            last[k] = d
     for k, d in last.items():
         if k.startswith("__amd"):
             continue
