@@ -517,8 +517,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   a.max_chunks = max_chunks;
   a.chunk_bits = cb;
   a.n_ck = n_ck;
-  a.emit_blocks = (uint32_t)(((uint64_t)max_chunks * (cb / DEC_EMIT_BITS) + 255) / 256);
-  a.chunk_blocks = (max_chunks + 255) / 256;
+  a.emit_blocks = (uint32_t)(((uint64_t)max_chunks * (cb / DEC_EMIT_BITS) + DEC_PARSE_THREADS - 1) / DEC_PARSE_THREADS);
+  a.chunk_blocks = (max_chunks + DEC_PARSE_THREADS - 1) / DEC_PARSE_THREADS;
   a.chunk_px = (unsigned long long*)(base + L.o_cpx);
   a.chunk_start = (unsigned long long*)(base + L.o_cstart);
   a.entry = (unsigned long long*)(base + L.o_entry);
@@ -559,7 +559,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
   for (uint32_t it = 0; it < queued; ++it, ++it_count) {
     tm.begin(NICE_PH_DEC_SYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
     tm.end(st);
   }
   NICE_HIP(hipMemcpyAsync(&host_changed, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
@@ -567,7 +567,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   for (uint32_t it = queued; host_changed && it < max_it; ++it, ++it_count) {
     NICE_HIP(hipMemsetAsync(changed + kSyncFlags - 1, 0, 4, st));
     tm.begin(NICE_PH_DEC_SYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(256), 0, st, a, changed + kSyncFlags - 1, nullptr);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + kSyncFlags - 1, nullptr);
     tm.end(st);
     NICE_HIP(hipMemcpyAsync(&host_changed, changed + kSyncFlags - 1, 4, hipMemcpyDeviceToHost, st));
     NICE_HIP(hipStreamSynchronize(st));
@@ -578,7 +578,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   tm.end(st);
   tm.begin(NICE_PH_DEC_EMIT, st);
   NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
-  hipLaunchKernelGGL(dec_emit, dim3(n_frames * a.emit_blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dec_emit, dim3(n_frames * a.emit_blocks), dim3(DEC_PARSE_THREADS), 0, st, a);
   tm.end(st);
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,

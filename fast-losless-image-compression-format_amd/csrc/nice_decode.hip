@@ -356,10 +356,11 @@ __device__ __forceinline__ uint32_t long_code(const LutLds& S, uint32_t v, uint3
   return ((uint32_t)S.sym[lo] << 5) | (uint32_t)S.len[lo];
 }
 
-// One symbol of stream st.
-__device__ __forceinline__ uint32_t dsym(Lane& L, const uint32_t* my, const LutLds& S, uint32_t st) {
+// One symbol of stream st (gp: S.gp[st], passed in for the prefix stream,
+// which a lane reads at every event).
+__device__ __forceinline__ uint32_t dsym_gp(Lane& L, const uint32_t* my, const LutLds& S, uint32_t st,
+                                            uint32_t gp) {
   const uint32_t v = (uint32_t)(L.win >> 32);
-  const uint32_t gp = S.gp[st];
   uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - ((gp >> 16) & 31u)))];
   if ((e & 31u) == 0) e = long_code(S, v, gp, S.gs[st]);
   const uint32_t n = e & 31u;
@@ -373,6 +374,9 @@ __device__ __forceinline__ uint32_t dsym(Lane& L, const uint32_t* my, const LutL
   L.rp += need ? 1u : 0u;
   L.avail += need ? 32u : 0u;
   return e >> 5;
+}
+__device__ __forceinline__ uint32_t dsym(Lane& L, const uint32_t* my, const LutLds& S, uint32_t st) {
+  return dsym_gp(L, my, S, st, S.gp[st]);
 }
 constexpr uint32_t PFX_STREAM = S_PREFIX;
 // payload stream i of mode m (code.rs:576-644), 4 bits each at 4 * (4m + i)
@@ -391,9 +395,9 @@ __device__ __forceinline__ uint32_t pay_stream(uint32_t m, uint32_t i) {
 
 // One pixel event at a prefix position: the prefix and, for a coded pixel, its
 // payload symbols.  Returns the prefix; s0..s3 receive the payload.
-__device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, const LutLds& S, uint32_t& s0,
-                                                uint32_t& s1, uint32_t& s2, uint32_t& s3) {
-  const uint32_t pfx = dsym(L, my, S, PFX_STREAM);
+__device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, const LutLds& S, uint32_t gp_pfx,
+                                                uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+  const uint32_t pfx = dsym_gp(L, my, S, PFX_STREAM, gp_pfx);
   if (pfx < (uint32_t)P_RUN1) {
     s0 = dsym(L, my, S, pay_stream(pfx, 0));
     if (pfx == (uint32_t)P_RGB || pfx == (uint32_t)P_LUMA || pfx == (uint32_t)P_LUMA2) {
@@ -455,9 +459,9 @@ __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
 // `prev`: the previous iteration's change flag -- when it is 0 the entries are
 // at the fixpoint already and this launch does nothing (the host queues several
 // iterations without waiting for each).
-__global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev) {
+__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev) {
   __shared__ LutLds S;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
   if (prev && *prev == 0) return;
   const uint32_t f = blockIdx.x / a.chunk_blocks;
   const uint32_t jb = blockIdx.x % a.chunk_blocks;
@@ -465,8 +469,8 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed, co
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
   const uint32_t nc = n_chunks(len, D, a.chunk_bits);
-  if (jb * 256u >= nc) return;
-  const uint32_t j = jb * 256u + threadIdx.x;
+  if (jb * DEC_PARSE_THREADS >= nc) return;
+  const uint32_t j = jb * DEC_PARSE_THREADS + threadIdx.x;
   const uint64_t base = (uint64_t)f * a.max_chunks;
   unsigned long long e = 0, last = ~0ull;
   if (j < nc) {
@@ -478,7 +482,8 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed, co
   load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
-  if (jb * 256u + wave * 64u >= nc) return;
+  if (jb * DEC_PARSE_THREADS + wave * 64u >= nc) return;
+  const uint32_t gp_pfx = S.gp[PFX_STREAM];
   uint32_t* wring = ring + wave * 64u * RING_STRIDE;
   const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
   const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(256) void dec_sync(DecArgs a, uint32_t* changed, co
     if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
     if (active) {
       uint32_t s0, s1, s2, s3;
-      const uint32_t pfx = pixel_event(L, my, S, s0, s1, s2, s3);
+      const uint32_t pfx = pixel_event(L, my, S, gp_pfx, s0, s1, s2, s3);
       px = sat_add(px, pixel_count(pfx, dk));
     }
   }
@@ -703,9 +708,9 @@ struct RecGroup {
 // converged parse's checkpoint (s * DEC_EMIT_BITS / 128 - 1) -- a prefix
 // position with its run digits and pixel count -- so emission parallelism does
 // not depend on the slice size the sync pass uses.
-__global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
+__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   __shared__ LutLds S;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 64 * RING_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
   const uint32_t f = blockIdx.x / a.emit_blocks;
   const uint32_t vb = blockIdx.x % a.emit_blocks;
   if (a.status[f] != 0) return;
@@ -714,12 +719,13 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
   const uint32_t nc = n_chunks(len, D, a.chunk_bits);
   const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS;
   const uint32_t nv = nc * subs;
-  if (vb * 256u >= nv) return;
+  if (vb * DEC_PARSE_THREADS >= nv) return;
   load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
-  if (vb * 256u + wave * 64u >= nv) return;
-  const uint32_t v = vb * 256u + threadIdx.x;
+  if (vb * DEC_PARSE_THREADS + wave * 64u >= nv) return;
+  const uint32_t gp_pfx = S.gp[PFX_STREAM];
+  const uint32_t v = vb * DEC_PARSE_THREADS + threadIdx.x;
   const uint32_t j = v / subs, sub = v - j * subs;
   uint32_t* wring = ring + wave * 64u * RING_STRIDE;
   const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
@@ -772,7 +778,7 @@ __global__ __launch_bounds__(256) void dec_emit(DecArgs a) {
     if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
     if (!active) continue;
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    const uint32_t pfx = pixel_event(L, my, S, s0, s1, s2, s3);
+    const uint32_t pfx = pixel_event(L, my, S, gp_pfx, s0, s1, s2, s3);
     if (at_n) {
       // the reference still reads one more prefix (code.rs:660): a run digit
       // there makes it copy past its buffer

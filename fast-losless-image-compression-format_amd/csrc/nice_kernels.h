@@ -56,6 +56,8 @@ struct EncArgs {
 __global__ void enc_classify(EncArgs a);
 __global__ void enc_classify_ring(EncArgs a);
 constexpr uint32_t CLS_RING_MAX_W = 5000;
+// dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
+constexpr uint32_t DEC_PARSE_THREADS = 512;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring
 __global__ void enc_tailruns(EncArgs a);
 __global__ void enc_tables(EncArgs a);
