@@ -1112,6 +1112,34 @@ __device__ __forceinline__ int rows_chain(IvS (&v)[S], IvS r0, IvS r1, IvS r2, c
   return go ? nlu : lu;
 }
 
+// rows_chain when every input is exact (r0..r2 and the kept pixels): plain
+// arithmetic, no intervals.  Only after the W_CUR words are resolved.
+__device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, uint32_t l3, uint32_t u,
+                                                    uint32_t wp) {
+  const uint32_t c = wp & SP_K;
+  const uint32_t va = ((((l1 + u) >> 1) & SP_K) + c) & SP_K;
+  const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
+  const uint32_t rlo = (sel + c) & SP_K;
+  return (wp & W_AVG) ? va : rlo;
+}
+template <int S>
+__device__ __forceinline__ int rows_chain_exact(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                                const uint32_t (&prev)[S], int lu, bool go) {
+  const int upto = go ? lu : -1;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    if (!__any(p <= upto)) break;
+    const uint32_t l1 = p >= 1 ? v[p - 1].lo : r0.lo;
+    const uint32_t l2 = p >= 2 ? v[p - 2].lo : (p == 1 ? r0.lo : r1.lo);
+    const uint32_t l3 = p >= 3 ? v[p - 3].lo : (p == 2 ? r0.lo : (p == 1 ? r1.lo : r2.lo));
+    const uint32_t n = rows_step_exact(l1, l2, l3, prev[p], w[p]);
+    const bool upd = p <= upto;
+    v[p].lo = upd ? n : v[p].lo;
+    v[p].len = upd ? 0u : v[p].len;
+  }
+  return go ? -1 : lu;
+}
+
 // Block barrier; with the ring in LDS only LDS traffic is ordered, so global
 // stores (the raster) and the record prefetch stay in flight across it.
 template <bool LDS_RING>
@@ -1256,7 +1284,10 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         exact_in = flags[lane - 1] != 0;
       }
       rows_barrier<LDS_RING>();
-      lu = rows_chain<S>(v, r0, r1, r2, w, prev, nvalid, lu, !fin);
+      if (__all(fin || exact_in))   // wave-uniform: every recomputing lane has exact inputs
+        lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, !fin);
+      else
+        lu = rows_chain<S>(v, r0, r1, r2, w, prev, nvalid, lu, !fin);
       if (!fin) {
         if (exact_in && lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         uint32_t* t = tails + lane * 6;
