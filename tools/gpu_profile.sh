@@ -16,9 +16,9 @@ cat $O/bench.json
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $S/kt -o run -- \
   python3 $R/bench.py --frames $FR --steps 3 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/kt.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $S/pmc_fetch -o run -- \
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "nice::" --output-format csv -d $S/pmc_fetch -o run -- \
   python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_fetch.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $S/pmc_write -o run -- \
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "nice::" --output-format csv -d $S/pmc_write -o run -- \
   python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_write.log 2>&1
 cd $R
 find $S -name "*.csv" -exec ls -la {} \; > $O/files.txt
