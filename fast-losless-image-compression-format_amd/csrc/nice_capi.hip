@@ -97,7 +97,7 @@ int check_device(int device) {
 static const char* kPhaseNames[NICE_PHASES] = {
     "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_tilebits", "enc_tilescan",
     "enc_pack", "enc_tail", "enc_serial", "dec_tables", "dec_sync", "dec_scan", "dec_emit",
-    "dec_reconstruct"};
+    "dec_reconstruct", "dec_place"};
 
 // Optional per-phase HIP-event timing (bench / profiling).
 struct PhaseTimer {
@@ -339,11 +339,13 @@ namespace {
 struct DecLayout {
   size_t total;
   size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
+  size_t o_ev, o_evck, o_evn, o_agree, o_items, o_icount;
 };
 // Jacobi iterations queued before the host first checks for the fixpoint (one
 // change flag each); further iterations, if any, check after every launch.
 constexpr uint32_t kSyncQueued = 6, kSyncFlags = 8;
-DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf) {
+DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf,
+                     uint32_t ev_cap, uint32_t subs) {
   DecLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -357,6 +359,13 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
   L.o_changed = take(4 * kSyncFlags);
   L.o_rowbuf = take(rowbuf);
+  // first-pass pixel events (ev_cap per slice, 0: not kept)
+  L.o_ev = take((size_t)n_frames * max_chunks * ev_cap * 4);
+  L.o_evck = take(ev_cap ? (size_t)n_frames * n_ck * max_chunks * 4 : 0);
+  L.o_evn = take(ev_cap ? (size_t)n_frames * max_chunks * 4 : 0);
+  L.o_agree = take(ev_cap ? (size_t)n_frames * max_chunks * 4 : 0);
+  L.o_items = take(ev_cap ? (size_t)n_frames * max_chunks * subs * 4 : 0);
+  L.o_icount = take(ev_cap ? (size_t)n_frames * 4 : 0);
   L.total = o;
   return L;
 }
@@ -496,8 +505,23 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
   const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 1) * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
-  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf);
+  // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
+  // a slice with more parses its events again in dec_emit) unless the scratch
+  // does not fit, then every slice is parsed again in dec_emit
+  uint32_t ev_cap = getenv("NICE_DEC_NO_EVENTS") ? 0u : cb / 4;
+  if (const char* ev = getenv("NICE_DEC_EV_CAP")) {   // tests: force event overflow
+    const uint32_t v = (uint32_t)atoi(ev);
+    if (ev_cap && v >= 4 && v % 4 == 0 && v < ev_cap) ev_cap = v;
+  }
+  const uint32_t subs = cb / DEC_EMIT_BITS;
+  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, ev_cap, subs);
   int rc = ctx->dec.grow(L.total);
+  if (rc && ev_cap) {
+    (void)hipGetLastError();   // the failed allocation
+    ev_cap = 0;
+    L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, 0, subs);
+    rc = ctx->dec.grow(L.total);
+  }
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->dec.ptr;
   DecArgs a{};
@@ -531,6 +555,15 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   a.rows_in_lds = g.in_lds ? 1u : 0u;
   a.rowbuf = (uint32_t*)(base + L.o_rowbuf);
   uint32_t* changed = (uint32_t*)(base + L.o_changed);
+  if (ev_cap) {
+    a.ev = (uint32_t*)(base + L.o_ev);
+    a.ev_cap = ev_cap;
+    a.ev_ck = (uint32_t*)(base + L.o_evck);
+    a.ev_n = (uint32_t*)(base + L.o_evn);
+    a.agree = (uint32_t*)(base + L.o_agree);
+    a.head_items = (uint32_t*)(base + L.o_items);
+    a.head_count = (uint32_t*)(base + L.o_icount);
+  }
 
   PhaseTimer& tm = ctx->timer;
   tm.begin(NICE_PH_DEC_TABLES, st);
@@ -577,9 +610,15 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
   tm.end(st);
   tm.begin(NICE_PH_DEC_EMIT, st);
+  if (a.ev) hipLaunchKernelGGL(dec_heads, dim3(n_frames), dim3(1024), 0, st, a);
   NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
   hipLaunchKernelGGL(dec_emit, dim3(n_frames * a.emit_blocks), dim3(DEC_PARSE_THREADS), 0, st, a);
   tm.end(st);
+  if (a.ev) {
+    tm.begin(NICE_PH_DEC_PLACE, st);
+    hipLaunchKernelGGL(dec_place, dim3((uint32_t)(((uint64_t)n_frames * max_chunks + 3) / 4)), dim3(256), 0, st, a);
+    tm.end(st);
+  }
   if (g.lds > 64 * 1024)
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
@@ -609,6 +648,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     fprintf(stderr, "\n");
     fprintf(stderr, "[nice dec stats] slice=%u emit waves=%llu wave_iters=%llu active_lane_iters=%llu fills=%llu\n",
             a.chunk_bits, h[20], h[16], h[17], h[18]);
+    fprintf(stderr, "[nice dec stats] slices by first-pass meeting checkpoint: 0:%llu 1:%llu 2-4:%llu 5-16:%llu "
+            "17-64:%llu 65+:%llu none:%llu overflow:%llu (ev_cap %u)\n",
+            h[50], h[51], h[52], h[53], h[54], h[55], h[56], h[57], a.ev_cap);
     fprintf(stderr, "[nice dec stats] fix-up rounds per row: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5:%llu 6+:%llu\n",
             h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
     (void)hipFree(dstats);

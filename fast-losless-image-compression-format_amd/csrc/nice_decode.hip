@@ -448,6 +448,13 @@ __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
   }
 }
 
+// Event word of a coded pixel: its prefix and payload symbols as read
+// (SMALL_DIFF index < 343, bytes < 256; LUMA: reference < 11, so its fourth
+// symbol fits bits 7..11); dec_place turns it into a record.
+__device__ __forceinline__ uint32_t ev_pack(uint32_t pfx, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
+  return pfx | (s0 << 3) | (s1 << 12) | (s2 << 20) | (pfx == (uint32_t)P_LUMA ? s3 << 7 : 0u);
+}
+
 // ---------------------------------------------------------------------------
 // D1: sync iteration (Jacobi, in place).  Each lane parses its slice from the
 // current entry guess and writes the exit as the next slice's entry.  Lanes
@@ -495,6 +502,11 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   const unsigned long long hard = len * 8 + 64;
   const uint32_t N = a.W * a.H;
   unsigned long long* ck = a.ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
+  // first pass: keep the pixel events (16-byte stores of 4)
+  const bool keep = a.ev != nullptr && !check;
+  uint32_t* evp = a.ev + (base + j) * a.ev_cap;
+  uint32_t* evck = a.ev_ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
+  uint32_t ne = 0, ev0 = 0, ev1 = 0, ev2 = 0;
   Lane L;
   L.pos = D + (e & ((1ull << 40) - 1));
   L.rp = RING_W;   // empty: filled on the first step
@@ -513,6 +525,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
         active = false;
       } else {
         ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
+        if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
         ++k;
         next_ck = k < a.n_ck ? next_ck + DEC_CK_BITS : ~0ull;
         ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
@@ -521,12 +534,37 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
     if (!__any(active)) break;
     if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
     if (active) {
-      uint32_t s0, s1, s2, s3;
+      uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
       const uint32_t pfx = pixel_event(L, my, S, gp_pfx, s0, s1, s2, s3);
-      px = sat_add(px, pixel_count(pfx, dk));
+      const uint32_t c = pixel_count(pfx, dk);
+      px = sat_add(px, c);
+      if (keep) {
+        const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
+        const uint32_t slot = ne & 3u;
+        if (ne < a.ev_cap && slot == 3u)
+          *reinterpret_cast<uint4*>(evp + ne - 3u) = make_uint4(ev0, ev1, ev2, ev);
+        ev0 = slot == 0u ? ev : ev0;
+        ev1 = slot == 1u ? ev : ev1;
+        ev2 = slot == 2u ? ev : ev2;
+        ++ne;
+      }
     }
   }
   if (!need) return;
+  if (keep) {
+    const uint32_t slot = ne & 3u, q0 = ne & ~3u;
+    if (ne <= a.ev_cap) {
+      if (slot > 0u) evp[q0] = ev0;
+      if (slot > 1u) evp[q0 + 1] = ev1;
+      if (slot > 2u) evp[q0 + 2] = ev2;
+    }
+    a.ev_n[base + j] = ne <= a.ev_cap ? ne : EV_OVERFLOW;
+    a.agree[base + j] = 0;
+  } else if (a.ev) {
+    // the final parse equals the first pass from the latest meeting point on
+    const uint32_t ag = synced ? k + 1u : AGREE_NONE;
+    a.agree[base + j] = max(a.agree[base + j], ag);
+  }
   if (a.stats && check) {   // diagnostics: where re-parses met the previous parse (16: never)
     atomicAdd(&a.stats[32 + (synced ? min(k, 15u) : 16u)], 1ull);
   }
@@ -647,18 +685,19 @@ constexpr unsigned long long CLS_PX_PACK = [] {
 }();
 
 
-// Record of a completed coded pixel (branch-free); `bad` when the reference
-// would panic on it (an index out of range or an offset before the image).
-__device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t mode, uint32_t s0,
-                                                uint32_t s1, uint32_t s2, uint32_t s3, bool& bad) {
+// Record of a completed coded pixel (branch-free), as an event word: the
+// record (bits 0..27) plus EV_L2 (LUMA2: needs the row above) and EV_BAD (an
+// index the reference rejects wherever the pixel is, or an offset that wraps
+// for W < 3).  The position-dependent checks are rec_bad_at's.
+__device__ __forceinline__ uint32_t make_event_rec(uint64_t W, uint32_t mode, uint32_t s0, uint32_t s1,
+                                                   uint32_t s2, uint32_t s3) {
   const bool isbr = mode == P_BACK_REF, islu = mode == P_LUMA;
   const bool issd = mode == P_SMALL_DIFF, isl2 = mode == P_LUMA2;
   const uint32_t id = min(isbr ? s0 : 5u + s0, 15u);
   const uint32_t cls = (uint32_t)(ID_CLS_PACK >> (4 * id)) & 15u;
   const uint64_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
   const int64_t off = (int64_t)(rows * W) + (int64_t)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;
-  // usize wrap (W < 3) or underflow before the image: the reference panics
-  const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0 >= 11u) || off < 0 || (int64_t)q < off;
+  const bool bad0 = (isbr && s0 >= 5u) || (islu && s0 >= 11u) || off < 0;
   const uint32_t gl = (s1 - 32u) & 255u;
   const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
   const uint32_t rd = s0 % 7u, t1 = s0 / 7u;
@@ -666,9 +705,22 @@ __device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t
   const uint32_t g2 = (s0 - 32u) & 255u;
   const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
   const uint32_t c_rgb = (s0 & 255u) | ((s1 & 255u) << 8) | ((s2 & 255u) << 16);
-  // LUMA2 needs the row above: position - channels*width underflows (code.rs:583)
-  bad = (isbr || islu) ? bad_ref : (isl2 && q < W);
-  return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+  const uint32_t r = (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+  return r | (isl2 ? EV_L2 : 0u) | ((isbr || islu) && bad0 ? EV_BAD : 0u);
+}
+// The reference panics on this pixel at position q: a reference before the
+// image start (code.rs:141-145 offsets) or LUMA2 on the first row (code.rs:583).
+__device__ __forceinline__ bool rec_bad_at(uint32_t ev, uint64_t q, uint64_t W) {
+  const uint32_t cls = (ev >> 24) & 15u;
+  const uint64_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
+  const uint64_t off = rows * W + ((CLS_PX_PACK >> (3 * cls)) & 7u) - 3u;   // >= 0 unless EV_BAD
+  return (ev & EV_BAD) || ((ev & EV_L2) ? q < W : (cls != 0u && q < off));
+}
+__device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t mode, uint32_t s0,
+                                                uint32_t s1, uint32_t s2, uint32_t s3, bool& bad) {
+  const uint32_t ev = make_event_rec(W, mode, s0, s1, s2, s3);
+  bad = rec_bad_at(ev, q, W);
+  return ev & 0x0FFFFFFFu;
 }
 
 struct RecGroup {
@@ -718,7 +770,8 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   const uint64_t D = a.data_start[f];
   const uint32_t nc = n_chunks(len, D, a.chunk_bits);
   const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS;
-  const uint32_t nv = nc * subs;
+  // with first-pass events kept, only the listed head sub-slices (dec_heads)
+  const uint32_t nv = a.head_items ? a.head_count[f] : nc * subs;
   if (vb * DEC_PARSE_THREADS >= nv) return;
   load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
@@ -726,7 +779,9 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   if (vb * DEC_PARSE_THREADS + wave * 64u >= nv) return;
   const uint32_t gp_pfx = S.gp[PFX_STREAM];
   const uint32_t v = vb * DEC_PARSE_THREADS + threadIdx.x;
-  const uint32_t j = v / subs, sub = v - j * subs;
+  const uint32_t item = !a.head_items ? v
+                      : v < nv ? a.head_items[(uint64_t)f * a.max_chunks * subs + v] : 0u;
+  const uint32_t j = item / subs, sub = item - j * subs;
   uint32_t* wring = ring + wave * 64u * RING_STRIDE;
   const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
   const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
@@ -757,6 +812,17 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
     const uint32_t c1 = (sub + 1) * step - 1;
     if (sub + 1 < subs && c1 < nvalid) end = begin + (ck[(uint64_t)c1 * a.max_chunks] & 0xFFFFu);
     if (q64 > N) active = false;      // past the image: tail bytes
+    if (a.ev) {
+      // dec_place writes the slice from where the final parse meets the first
+      // pass (its events kept): this lane only parses the head before that
+      const uint32_t ag = a.agree[base + j];
+      if (ag != AGREE_NONE && a.ev_n[base + j] != EV_OVERFLOW && ag <= nvalid) {
+        const unsigned long long stop =
+            ag == 0u ? begin : begin + (ck[(uint64_t)(ag - 1u) * a.max_chunks] & 0xFFFFu);
+        if (stop < end) end = stop;
+        if (sub * step >= ag) active = false;   // starts at or past the meeting point
+      }
+    }
   }
   uint32_t q = (uint32_t)(q64 > N ? N : q64);
   const uint32_t q0 = q;
@@ -803,6 +869,151 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
     }
   }
   G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
+  if (err) set_status(&a.status[f], NICE_E_FORMAT);
+}
+
+// ---------------------------------------------------------------------------
+// D4a: list the sub-slices dec_emit parses (one 1024-thread block per frame):
+// each slice's head before the checkpoint where the final parse meets the
+// first pass, or the whole slice when it never does (or its events
+// overflowed).  Compact lists keep dec_emit's waves full of working lanes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void dec_heads(DecArgs a) {
+  __shared__ uint32_t part[1024];
+  const uint32_t f = blockIdx.x;
+  if (a.status[f] != 0) {
+    if (threadIdx.x == 0) a.head_count[f] = 0;
+    return;
+  }
+  const uint32_t nc = n_chunks(a.stream_len[f], a.data_start[f], a.chunk_bits);
+  const uint64_t base = (uint64_t)f * a.max_chunks;
+  const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS, step = DEC_EMIT_BITS / DEC_CK_BITS;
+  const uint32_t per = (nc + 1023) / 1024;
+  const uint32_t c0 = min(threadIdx.x * per, nc), c1 = min(c0 + per, nc);
+  auto nsub = [&](uint32_t j) -> uint32_t {
+    const uint32_t ag = a.agree[base + j], nvalid = (uint32_t)(a.last[base + j] >> 56);
+    if (ag == AGREE_NONE || a.ev_n[base + j] == EV_OVERFLOW || ag > nvalid)
+      return min(subs, 1u + nvalid / step);   // every sub-slice with a start (s * step - 1 < nvalid)
+    return (ag + step - 1) / step;            // sub-slices starting before the meeting point
+  };
+  uint32_t cnt = 0;
+  for (uint32_t j = c0; j < c1; ++j) cnt += nsub(j);
+  part[threadIdx.x] = cnt;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t t = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t o = part[threadIdx.x] - cnt;
+  uint32_t* items = a.head_items + base * subs;
+  for (uint32_t j = c0; j < c1; ++j) {
+    const uint32_t n = nsub(j);
+    for (uint32_t s = 0; s < n; ++s) items[o++] = j * subs + s;
+  }
+  if (threadIdx.x == 1023) a.head_count[f] = part[1023];
+}
+
+// ---------------------------------------------------------------------------
+// D4b: place the first pass's events past each slice's meeting point (one wave
+// per slice): pixel positions by a wave prefix sum of the events' pixel
+// counts, one coalesced 4-byte record store per coded pixel, runs left to the
+// memset marker.  Same checks as dec_emit: the first event at q == N is the
+// extra prefix the reference reads (strict: a run digit there is an error),
+// a run past N or a reference the reference rejects sets NICE_E_FORMAT.
+// ---------------------------------------------------------------------------
+// Inclusive wave64 prefix sum by DPP: shifts 1, 2, 4, 8 inside each row of 16
+// lanes, then row 15 -> rows 1 and 3, row 31 -> rows 2 and 3.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return v;
+}
+
+__global__ __launch_bounds__(256) void dec_place(DecArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t sl = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t f = (uint32_t)(sl / a.max_chunks), j = (uint32_t)(sl % a.max_chunks);
+  if (f >= a.n_frames || a.status[f] != 0) return;
+  const uint64_t len = a.stream_len[f];
+  const uint64_t D = a.data_start[f];
+  if (j >= n_chunks(len, D, a.chunk_bits)) return;
+  const uint64_t base = (uint64_t)f * a.max_chunks;
+  const uint32_t ag = a.agree[base + j], nev = a.ev_n[base + j];
+  const uint32_t nvalid = (uint32_t)(a.last[base + j] >> 56);
+  if (a.stats && lane == 0) {   // diagnostics: where the final parse met the first pass
+    const uint32_t b = nev == EV_OVERFLOW ? 7u : ag == AGREE_NONE ? 6u : ag == 0u ? 0u : ag == 1u ? 1u
+                     : ag <= 4u ? 2u : ag <= 16u ? 3u : ag <= 64u ? 4u : 5u;
+    atomicAdd(&a.stats[50 + b], 1ull);
+  }
+  if (ag == AGREE_NONE || nev == EV_OVERFLOW || ag > nvalid) return;   // dec_emit parsed it all
+  const uint64_t cki = (uint64_t)f * a.n_ck * a.max_chunks + j + (uint64_t)(ag ? ag - 1u : 0u) * a.max_chunks;
+  const uint32_t i_first = ag == 0u ? 0u : a.ev_ck[cki];
+  unsigned long long q = a.chunk_start[base + j] + (ag == 0u ? 0ull : (a.ck[cki] >> 32));
+  const uint64_t N = (uint64_t)a.W * a.H;
+  if (q > N) return;                    // tail bytes
+  const uint32_t* evp = a.ev + (base + j) * a.ev_cap;
+  uint32_t* rec = a.recs + (uint64_t)f * a.rec_stride;
+  const bool strict = (a.flags & NICE_DEC_STRICT_REFERENCE) != 0;
+  bool err = false;
+  // 256 events per step: 4 rows of 64 consecutive events (coalesced loads and
+  // record stores), prefix sums per row plus the rows before
+  for (uint32_t i = i_first; i < nev; i += 256u) {
+    uint32_t ev[4], r[4];
+    unsigned long long c[4], qk[4], carry = 0;
+    uint32_t stop_k = 4u, stop_lane = 64u;
+    bool stop_at_n = false, stop_run = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = i + 64u * k + lane;
+      const bool valid = x < nev;
+      ev[k] = valid ? evp[x] : 0u;
+      const bool run = (ev[k] & EV_RUN) != 0u;
+      c[k] = valid ? (run ? (ev[k] & ~EV_RUN) : 1u) : 0u;
+      unsigned long long incl;
+      if (!__any(c[k] >= (1u << 25))) {   // 64 counts < 2^25: a 32-bit scan
+        incl = wave_incl_scan((uint32_t)c[k]);
+      } else {
+        incl = c[k];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned long long t = __shfl_up(incl, o);
+          if ((int)lane >= o) incl += t;
+        }
+      }
+      const unsigned long long qb = q + carry + incl - c[k];   // pixels before this event
+      carry += __shfl(incl, 63);
+      qk[k] = qb;
+      const uint32_t pfx = ev[k] & 7u;
+      bool rbad = false;
+      r[k] = make_record(a.W, qb, pfx, (ev[k] >> 3) & (pfx == (uint32_t)P_LUMA ? 15u : 511u),
+                         (ev[k] >> 12) & 255u, (ev[k] >> 20) & 255u, (ev[k] >> 7) & 31u, rbad);
+      const bool at_n = valid && qb == N;
+      const bool bad = valid && !at_n && (run ? qb + c[k] > N : rbad);
+      const unsigned long long m = __ballot(at_n || bad);
+      if (stop_k == 4u && m) {
+        stop_k = (uint32_t)k;
+        stop_lane = (uint32_t)__builtin_ctzll(m);
+        stop_at_n = __shfl(at_n ? 1 : 0, (int)stop_lane) != 0;
+        stop_run = __shfl(run ? 1 : 0, (int)stop_lane) != 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool keep = (uint32_t)k < stop_k || ((uint32_t)k == stop_k && lane < stop_lane);
+      if (keep && i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qk[k]] = r[k];
+    }
+    if (stop_k < 4u) {
+      if (lane == 0) err = stop_at_n ? (strict && stop_run) : true;
+      break;
+    }
+    q += carry;
+  }
   if (err) set_status(&a.status[f], NICE_E_FORMAT);
 }
 

@@ -110,13 +110,28 @@ struct DecArgs {
   uint32_t rows_in_lds;               // 1: row ring in LDS, 0: in rowbuf
   uint32_t* rowbuf;                   // n_frames * R * W (when not in LDS)
   unsigned long long* stats;          // optional diagnostics (NICE_DEC_STATS=1), else null
+  // pixel events of the first sync pass, reused past the point where the final
+  // parse meets it (dec_place); null: not kept (dec_emit parses every slice)
+  uint32_t* ev;                       // n_frames * max_chunks * ev_cap events
+  uint32_t ev_cap;                    // events per slice (multiple of 4)
+  uint32_t* ev_ck;                    // n_frames * n_ck * max_chunks: events before checkpoint k (first pass)
+  uint32_t* ev_n;                     // n_frames * max_chunks: events of the first pass, EV_OVERFLOW
+  uint32_t* agree;                    // n_frames * max_chunks: final parse == first pass from checkpoint agree-1 (0: entry)
+  uint32_t* head_items;               // n_frames * max_chunks * (chunk_bits / DEC_EMIT_BITS): dec_emit's sub-slices
+  uint32_t* head_count;               // n_frames: sub-slices listed
 };
+// event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
+// EV_RUN | pixels (saturated)
+constexpr uint32_t EV_RUN = 1u << 31, EV_BAD = 1u << 29, EV_L2 = 1u << 28;
+constexpr uint32_t EV_OVERFLOW = 0xFFFFFFFFu, AGREE_NONE = 0xFFFFu;
 
 __global__ void dec_tables(DecArgs a);
 __global__ void dec_init_entries(DecArgs a);
 __global__ void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev);
 __global__ void dec_scan(DecArgs a);
 __global__ void dec_emit(DecArgs a);
+__global__ void dec_place(DecArgs a);
+__global__ void dec_heads(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);
 __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);

@@ -156,6 +156,29 @@ def test_decode_long_slices(nice, O, bits, monkeypatch):
         assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), name
 
 
+@pytest.mark.parametrize("mode", [("NICE_DEC_NO_EVENTS", "1"), ("NICE_DEC_EV_CAP", "16"),
+                                  ("NICE_DEC_EV_CAP", "64")])
+@pytest.mark.parametrize("bits", [1024, 4096])
+def test_decode_event_paths(nice, O, mode, bits, monkeypatch):
+    """Record emission without the first pass's events (every slice parsed again)
+    and with a capacity so small that most slices overflow (mixed paths)."""
+    monkeypatch.setenv(*mode)
+    monkeypatch.setenv("NICE_DEC_SLICE_BITS", str(bits))
+    for name, px, w, h, c in CASES:
+        if name not in ("syn512x4", "syn1920x1080x4", "stripes700x300x3", "noise300x200x3", "odd37x23x4"):
+            continue
+        s = O.encode(px, w, h, c)
+        try:
+            O.decode(s, O.DEC_STRIDE)
+        except O.OracleDecodeError:
+            with pytest.raises(nice.NiceError):
+                nice.decode_bytes(s)
+            continue
+        got, _ = nice.decode_bytes(s)
+        g = np.frombuffer(got, np.uint8).reshape(-1, c)
+        assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), (name, mode, bits)
+
+
 def test_decode_single_wave_rows(nice, O, monkeypatch):
     """The single-wave row kernel (used for W < 64 or W > 16384) on wide images."""
     monkeypatch.setenv("NICE_DEC_SINGLE_WAVE", "1")
