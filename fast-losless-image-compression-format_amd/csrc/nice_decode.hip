@@ -923,6 +923,35 @@ __global__ __launch_bounds__(1024) void dec_heads(DecArgs a) {
 // extra prefix the reference reads (strict: a run digit there is an error),
 // a run past N or a reference the reference rejects sets NICE_E_FORMAT.
 // ---------------------------------------------------------------------------
+// make_record for dec_place: 32-bit arithmetic (q <= N <= 2^30, 3W < 2^32),
+// the SMALL_DIFF constant from a table (sdl: 343 packed constants in LDS).
+constexpr uint32_t ID_CLS_LO = (uint32_t)ID_CLS_PACK, ID_CLS_HI = (uint32_t)(ID_CLS_PACK >> 32);
+constexpr uint32_t CLS_PX_LO = (uint32_t)CLS_PX_PACK, CLS_PX_HI = (uint32_t)(CLS_PX_PACK >> 32);
+__device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32_t W, const uint32_t* sdl,
+                                                 bool& bad) {
+  const uint32_t pfx = ev & 7u;
+  const bool isbr = pfx == (uint32_t)P_BACK_REF, islu = pfx == (uint32_t)P_LUMA;
+  const bool issd = pfx == (uint32_t)P_SMALL_DIFF, isl2 = pfx == (uint32_t)P_LUMA2;
+  const uint32_t s0 = (ev >> 3) & 511u, s1 = (ev >> 12) & 255u, s2 = (ev >> 20) & 255u, s3 = (ev >> 7) & 31u;
+  const uint32_t s0l = s0 & 15u;   // LUMA: the reference (bits 3..6)
+  const uint32_t id = min(isbr ? s0 : 5u + s0l, 15u);
+  const uint32_t cls = (id < 8u ? ID_CLS_LO >> (4u * id) : ID_CLS_HI >> (4u * id - 32u)) & 15u;
+  const uint32_t rows = (CLS_ROWS_PACK >> (2u * cls)) & 3u;
+  const uint32_t b3 = 3u * cls;   // px + 3 at bits 3cls (48 bits over two words)
+  const uint32_t pxp = (b3 < 32u ? (CLS_PX_LO >> b3) | (b3 > 29u ? CLS_PX_HI << (32u - b3) : 0u)
+                                 : CLS_PX_HI >> (b3 - 32u)) & 7u;
+  const uint32_t off3 = rows * W + pxp;   // offset + 3
+  const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0l >= 11u) || off3 < 3u || q + 3u < off3;
+  const uint32_t gl = (s1 - 32u) & 255u;
+  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
+  const uint32_t c_sd = sdl[min(s0, 342u)];
+  const uint32_t g2 = (s0 - 32u) & 255u;
+  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
+  const uint32_t c_rgb = (s0 & 255u) | (s1 << 8) | (s2 << 16);
+  bad = (isbr || islu) ? bad_ref : (isl2 && q < W);
+  return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+}
+
 // Inclusive wave64 prefix sum by DPP: shifts 1, 2, 4, 8 inside each row of 16
 // lanes, then row 15 -> rows 1 and 3, row 31 -> rows 2 and 3.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -936,6 +965,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 }
 
 __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
+  __shared__ uint32_t sdl[343];   // SMALL_DIFF index -> constant (code.rs:230-247)
+  for (uint32_t i = threadIdx.x; i < 343u; i += 256u) {
+    const uint32_t rd = i % 7u, t1 = i / 7u;
+    sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
+  }
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t sl = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t f = (uint32_t)(sl / a.max_chunks), j = (uint32_t)(sl % a.max_chunks);
@@ -963,8 +998,17 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
   bool err = false;
   // 256 events per step: 4 rows of 64 consecutive events (coalesced loads and
   // record stores), prefix sums per row plus the rows before
+  uint32_t nx[4];   // the next step's events, loaded one step ahead
+#pragma unroll
+  for (int k = 0; k < 4; ++k) nx[k] = i_first + 64u * k + lane < nev ? evp[i_first + 64u * k + lane] : 0u;
   for (uint32_t i = i_first; i < nev; i += 256u) {
     uint32_t ev[4], r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ev[k] = nx[k];
+      const uint32_t y = i + 256u + 64u * k + lane;
+      nx[k] = y < nev ? evp[y] : 0u;
+    }
     unsigned long long c[4], qk[4], carry = 0;
     uint32_t stop_k = 4u, stop_lane = 64u;
     bool stop_at_n = false, stop_run = false;
@@ -972,7 +1016,6 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
     for (int k = 0; k < 4; ++k) {
       const uint32_t x = i + 64u * k + lane;
       const bool valid = x < nev;
-      ev[k] = valid ? evp[x] : 0u;
       const bool run = (ev[k] & EV_RUN) != 0u;
       c[k] = valid ? (run ? (ev[k] & ~EV_RUN) : 1u) : 0u;
       unsigned long long incl;
@@ -989,10 +1032,8 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
       const unsigned long long qb = q + carry + incl - c[k];   // pixels before this event
       carry += __shfl(incl, 63);
       qk[k] = qb;
-      const uint32_t pfx = ev[k] & 7u;
       bool rbad = false;
-      r[k] = make_record(a.W, qb, pfx, (ev[k] >> 3) & (pfx == (uint32_t)P_LUMA ? 15u : 511u),
-                         (ev[k] >> 12) & 255u, (ev[k] >> 20) & 255u, (ev[k] >> 7) & 31u, rbad);
+      r[k] = place_record(ev[k], (uint32_t)min(qb, N), a.W, sdl, rbad);
       const bool at_n = valid && qb == N;
       const bool bad = valid && !at_n && (run ? qb + c[k] > N : rbad);
       const unsigned long long m = __ballot(at_n || bad);
