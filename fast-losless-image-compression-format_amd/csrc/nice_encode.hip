@@ -1058,33 +1058,41 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
 
 // Tile bits from the per-tile symbol counts of enc_classify_ring: sum of
 // count x code length over the 858 bins, plus the run digits of the tile's
-// last run (it ends at tile_next, in a later tile; code.rs:371-407).
+// last run (it ends at tile_next, in a later tile; code.rs:371-407).  One wave
+// per tile, no block barriers: each wave keeps the code lengths of its current
+// frame in its own LDS slice.
 __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
-  __shared__ uint32_t lens[2 * TH_WORDS];
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t lens_all[4][2 * TH_WORDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* lens = lens_all[wid];
   const uint32_t T = a.tiles_per_frame;
   uint32_t cur_f = 0xFFFFFFFFu;
   uint64_t t0, t1;
   tile_range(a, t0, t1);
-  for (uint64_t w = t0; w < t1; ++w) {
+  for (uint64_t w = t0 + wid; w < t1; w += 4) {
     const uint64_t t = work_tile(a, w);
     const uint32_t f = (uint32_t)(t / T);
-    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
+    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // wave-uniform
     if (f != cur_f) {
-      __syncthreads();
-      for (int b = threadIdx.x; b < (int)(2 * TH_WORDS); b += 256)
+      __builtin_amdgcn_wave_barrier();
+      for (int b = lane; b < (int)(2 * TH_WORDS); b += 64)
         lens[b] = b < N_BINS ? (a.tbl[(uint64_t)f * N_BINS + b] & 31u) : 0u;
       cur_f = f;
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
     const uint32_t* th = a.tile_hist + t * TH_WORDS;
     uint32_t acc = 0;
-    for (int k = threadIdx.x; k < (int)TH_WORDS; k += 256) {
-      const uint32_t v = th[k];
-      acc += (v & 0xFFFFu) * lens[2 * k] + (v >> 16) * lens[2 * k + 1];
+#pragma unroll
+    for (int k0 = 0; k0 < (int)TH_WORDS; k0 += 64) {
+      const int k = k0 + lane;
+      if (k < (int)TH_WORDS) {
+        const uint32_t v = th[k];
+        acc += (v & 0xFFFFu) * lens[2 * k] + (v >> 16) * lens[2 * k + 1];
+      }
     }
-    if (threadIdx.x == 0) {
+    if (lane == 0) {
       const uint32_t last = a.tile_last[t];
       if (last != NONE) {
         const uint64_t run = (uint64_t)a.tile_next[t] - last - 1;
@@ -1100,10 +1108,7 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-    __syncthreads();
-    if (lane == 0) wsum[wid] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) a.tile_bits[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (lane == 0) a.tile_bits[t] = acc;
   }
 }
 
@@ -1145,7 +1150,7 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   }
 }
 
-__global__ __launch_bounds__(ENC_THREADS) void enc_pack(EncArgs a) {
+__global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
