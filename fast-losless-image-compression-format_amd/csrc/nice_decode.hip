@@ -952,18 +952,6 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
   return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
 }
 
-// Inclusive wave64 prefix sum by DPP: shifts 1, 2, 4, 8 inside each row of 16
-// lanes, then row 15 -> rows 1 and 3, row 31 -> rows 2 and 3.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
-  return v;
-}
-
 __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
   __shared__ uint32_t sdl[343];   // SMALL_DIFF index -> constant (code.rs:230-247)
   for (uint32_t i = threadIdx.x; i < 343u; i += 256u) {

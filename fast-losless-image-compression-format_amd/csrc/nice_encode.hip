@@ -959,10 +959,7 @@ __device__ __forceinline__ void quad_mask(const uint32_t (&rc)[4], int lane, int
   Q.nib = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) Q.nib |= ((Q.rc[q] & 7u) != REC_UNCODED ? 1u : 0u) << q;
-  uint32_t mw = Q.nib << (4 * (lane & 7));
-  mw |= __shfl_xor(mw, 1);
-  mw |= __shfl_xor(mw, 2);
-  mw |= __shfl_xor(mw, 4);
+  const uint32_t mw = wave_or8(Q.nib << (4 * (lane & 7)));
   if ((lane & 7) == 0) mask[wid * 8 + (lane >> 3)] = mw;
 }
 
@@ -1184,11 +1181,7 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
     quad_bits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
-    uint32_t x = Q.nb;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y2 = __shfl_up(x, o);
-      if (lane >= o) x += y2;
-    }
+    const uint32_t x = wave_incl_scan(Q.nb);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     uint32_t wbase = 0, tile_bits = 0;

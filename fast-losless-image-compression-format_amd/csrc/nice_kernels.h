@@ -136,4 +136,25 @@ __global__ void dec_reconstruct(DecArgs a);
 __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);
 
+// Inclusive wave64 prefix sum by DPP: shifts 1, 2, 4, 8 inside each row of 16
+// lanes, then row 15 -> rows 1 and 3, row 31 -> rows 2 and 3.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return v;
+}
+
+// OR over each aligned group of 8 lanes (quad xor 1, xor 2, then the other
+// quad of the group by row_half_mirror).
+__device__ __forceinline__ uint32_t wave_or8(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+  return v;
+}
+
 }  // namespace nice
