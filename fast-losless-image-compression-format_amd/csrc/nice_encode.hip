@@ -207,6 +207,21 @@ __device__ __forceinline__ uint32_t rec_bins(const RecBinTable& t, uint32_t rec,
   return r.x >> 20;
 }
 
+// Work item -> (frame, tile) without a 64-bit division per tile (one at the
+// start; the scalar division sequence is ~100 instructions).
+struct TileIter {
+  uint32_t f, k, nt, lo, T;
+  __device__ __forceinline__ TileIter(const EncArgs& a, uint64_t w)
+      : f((uint32_t)(w / (a.tile_hi - a.tile_lo))), k((uint32_t)(w % (a.tile_hi - a.tile_lo))),
+        nt(a.tile_hi - a.tile_lo), lo(a.tile_lo), T(a.tiles_per_frame) {}
+  __device__ __forceinline__ void step(uint32_t n) {
+    k += n;
+    while (k >= nt) { k -= nt; ++f; }
+  }
+  __device__ __forceinline__ uint32_t tt() const { return lo + k; }
+  __device__ __forceinline__ uint64_t tile() const { return (uint64_t)f * T + lo + k; }
+};
+
 // Branch-free mode decision for a pixel whose every reference exists
 // (i >= 3W+3, W >= 3): all tests are evaluated and the first hit in the
 // reference order wins (code.rs:191-366).  Neighbours come from the LDS windows
@@ -518,9 +533,9 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   }
   // the first tile's pixels
   uint32_t pf[CLS_PPT];
-  auto fetch = [&](uint64_t w, uint32_t (&v)[CLS_PPT]) {
-    const uint32_t f = (uint32_t)(w / T);
-    const int64_t start = (int64_t)(w % T) * ENC_TILE;
+  auto fetch = [&](const TileIter& ti, uint32_t (&v)[CLS_PPT]) {
+    const uint32_t f = ti.f;
+    const int64_t start = (int64_t)ti.tt() * ENC_TILE;
     const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
@@ -528,10 +543,11 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       v[q] = j < N ? fr[j] : 0u;
     }
   };
-  fetch(w_begin, pf);
-  for (uint64_t w = w_begin; w < w_end; ++w) {
-    const uint32_t f = (uint32_t)(w / T);
-    const uint32_t tt = (uint32_t)(w % T);
+  TileIter it(a, w_begin), nx(a, w_begin);
+  fetch(nx, pf);
+  for (uint64_t w = w_begin; w < w_end; ++w, it.step(1)) {
+    const uint32_t f = it.f;
+    const uint32_t tt = it.tt();
     if (f != cur_frame) { flush(cur_frame); cur_frame = f; }
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)min((int64_t)ENC_TILE, N - start);
@@ -542,7 +558,8 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       ring[k] = y;
       if (k < CLS_GUARD) ring[CLS_RING + k] = y;
     }
-    if (w + 1 < w_end) fetch(w + 1, pf);
+    nx.step(1);
+    if (w + 1 < w_end) fetch(nx, pf);
     __syncthreads();
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
@@ -934,9 +951,7 @@ struct TileQuad {
 
 // The thread's 4 records of tile t (REC_UNCODED past the frame end); issued one
 // tile ahead so the loads overlap the previous tile's work.
-__device__ __forceinline__ void quad_fetch(const EncArgs& a, uint64_t t, int p0, uint32_t (&rc)[4]) {
-  const uint32_t T = a.tiles_per_frame;
-  const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+__device__ __forceinline__ void quad_fetch(const EncArgs& a, uint32_t f, uint32_t tt, int p0, uint32_t (&rc)[4]) {
   const int64_t N = (int64_t)a.W * a.H;
   const int64_t start = (int64_t)tt * ENC_TILE;
   const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
@@ -1010,10 +1025,6 @@ __device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& w0, uint6
   w0 = (uint64_t)blockIdx.x * per;
   w1 = w0 + per < total ? w0 + per : total;
 }
-__device__ __forceinline__ uint64_t work_tile(const EncArgs& a, uint64_t w) {
-  const uint32_t nt = a.tile_hi - a.tile_lo;
-  return (w / nt) * a.tiles_per_frame + a.tile_lo + (uint32_t)(w % nt);
-}
 
 __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   __shared__ uint32_t tbl[N_BINS];
@@ -1029,12 +1040,14 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   uint64_t t0, t1;
   tile_range(a, t0, t1);
   uint32_t rn[4];
-  if (t0 < t1) quad_fetch(a, work_tile(a, t0), p0, rn);
-  for (uint64_t w = t0; w < t1; ++w) {
-    const uint64_t t = work_tile(a, w);
+  TileIter it(a, t0), nx(a, t0);
+  if (t0 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
+  for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
+    const uint64_t t = it.tile();
     uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    if (w + 1 < t1) quad_fetch(a, work_tile(a, w + 1), p0, rn);
-    const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+    nx.step(1);
+    if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
+    const uint32_t f = it.f, tt = it.tt();
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
@@ -1066,9 +1079,10 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
   uint32_t cur_f = 0xFFFFFFFFu;
   uint64_t t0, t1;
   tile_range(a, t0, t1);
-  for (uint64_t w = t0 + wid; w < t1; w += 4) {
-    const uint64_t t = work_tile(a, w);
-    const uint32_t f = (uint32_t)(t / T);
+  TileIter it(a, t0 + wid);
+  for (uint64_t w = t0 + wid; w < t1; w += 4, it.step(4)) {
+    const uint64_t t = it.tile();
+    const uint32_t f = it.f;
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // wave-uniform
     if (f != cur_f) {
       __builtin_amdgcn_wave_barrier();
@@ -1165,12 +1179,14 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
   tile_range(a, t0, t1);
   (void)total;
   uint32_t rn[4];
-  if (t0 < t1) quad_fetch(a, work_tile(a, t0), p0, rn);
-  for (uint64_t w = t0; w < t1; ++w) {
-    const uint64_t t = work_tile(a, w);
+  TileIter it(a, t0), nx(a, t0);
+  if (t0 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
+  for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
+    const uint64_t t = it.tile();
     uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    if (w + 1 < t1) quad_fetch(a, work_tile(a, w + 1), p0, rn);
-    const uint32_t f = (uint32_t)(t / T), tt = (uint32_t)(t % T);
+    nx.step(1);
+    if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
+    const uint32_t f = it.f, tt = it.tt();
     if (a.frame_flags[f] & FLAG_SERIAL) continue;   // enc_serial's frame
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
