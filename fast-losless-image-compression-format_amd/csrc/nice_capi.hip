@@ -616,7 +616,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   tm.end(st);
   if (a.ev) {
     tm.begin(NICE_PH_DEC_PLACE, st);
-    hipLaunchKernelGGL(dec_place, dim3((uint32_t)(((uint64_t)n_frames * max_chunks + 3) / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(dec_place, dim3((max_chunks + 3) / 4, n_frames), dim3(256), 0, st, a);
     tm.end(st);
   }
   if (g.lds > 64 * 1024)

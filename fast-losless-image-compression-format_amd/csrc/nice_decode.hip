@@ -960,9 +960,8 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t sl = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-  const uint32_t f = (uint32_t)(sl / a.max_chunks), j = (uint32_t)(sl % a.max_chunks);
-  if (f >= a.n_frames || a.status[f] != 0) return;
+  const uint32_t f = blockIdx.y, j = blockIdx.x * 4u + (threadIdx.x >> 6);   // grid (slices / 4, frames)
+  if (a.status[f] != 0) return;
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
   if (j >= n_chunks(len, D, a.chunk_bits)) return;
