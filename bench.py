@@ -87,6 +87,33 @@ def cpu_baseline(W, H, seconds=12.0):
                       f"{t_total:.1f} s single-thread"}
 
 
+def cpu_baseline_threads(W, H, seconds=8.0):
+    """The same oracle work frame-parallel on the host's CPU share (SURVEY.md
+    §8d: per-image 1-thread time and frame-parallel throughput): one frame per
+    thread per round, the C calls release the GIL."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    frames = [O.gen_syn_v1(W, H, 4, seed) for seed in range(1, threads + 1)]
+
+    def work(px):
+        s3 = bytearray(O.encode(px, W, H, 4))
+        s3[12] = 3
+        O.decode(bytes(s3))
+
+    n = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(work, frames))
+            n += threads
+    el = time.perf_counter() - t0
+    return {"value": round(n * W * H / el / 1e6, 3), "unit": "MPixels/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} x {W}x{H} RGBA NICE-SYN-v1 frames ({threads} distinct, seeds 1..{threads}), "
+                      f"encode+decode, {threads} threads, {el:.1f} s"}
+
+
 def timed_region(step, steps, sync, barrier):
     """Barrier + sync on both sides of exactly `steps` calls of `step`."""
     barrier()
@@ -348,9 +375,11 @@ def main():
         "sharded_image_encode": sharded,
         "streamed_host_frames": stream_leg,
         "cpu_baseline": None,
+        "cpu_baseline_threads": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(W, H, args.cpu_seconds)
+        res["cpu_baseline_threads"] = cpu_baseline_threads(W, H, min(args.cpu_seconds, 8.0))
     if rank == 0:
         print(json.dumps(res))
     if dist is not None:
