@@ -309,6 +309,9 @@ def main():
     one_d, one_st = dec[:1], status[:1]
     t_one = timed(lambda: (nice.encode_batch(one_px, W, H, 4, one_s, one_l),
                            nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st)), reps=2)
+    # measured copy peak: device-to-device copy of the frames
+    t_copy = timed(lambda: dec.copy_(px), reps=3)
+    copy_gb_s = 2 * px.numel() / t_copy / 1e9
 
     sharded = None
     if world > 1 and args.sharded_side:
@@ -358,6 +361,7 @@ def main():
                    "channels": 4, "frames_per_gpu_per_step": F,
                    "parallelism": f"frames sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "copy_peak_measured": round(copy_gb_s, 1),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": round(achieved * 1e9 / HBM_PEAK, 5),
                      "traffic": load_traffic(dom, F),
