@@ -1033,7 +1033,6 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   __shared__ RecBinTable rbt;
   rbt_init(rbt, threadIdx.x);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t T = a.tiles_per_frame;
   const int64_t N = (int64_t)a.W * a.H;
   const int p0 = 4 * threadIdx.x;
   uint32_t cur_f = 0xFFFFFFFFu;
@@ -1075,7 +1074,6 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
   __shared__ uint32_t lens_all[4][2 * TH_WORDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t* lens = lens_all[wid];
-  const uint32_t T = a.tiles_per_frame;
   uint32_t cur_f = 0xFFFFFFFFu;
   uint64_t t0, t1;
   tile_range(a, t0, t1);

@@ -26,6 +26,9 @@ def _frames():
         ("grad64x48x3", O.gen_gradient(64, 48, 3), 64, 48, 3),
         ("odd37x23x4", O.gen_syn_v1(37, 23, 4, 9), 37, 23, 4),
         ("wide1000x7x3", O.gen_syn_v1(1000, 7, 3, 5), 1000, 7, 3),
+        # W > 5000: window classify (no LDS ring); W > 8192: row decode with its ring in global memory
+        ("wide6000x12x4", O.gen_syn_v1(6000, 12, 4, 6), 6000, 12, 4),
+        ("wide9000x6x3", O.gen_syn_v1(9000, 6, 3, 7), 9000, 6, 3),
         ("noise300x200x3", rng.integers(0, 256, 300 * 200 * 3, dtype=np.uint8), 300, 200, 3),
         ("noise128x128x4", rng.integers(0, 256, 128 * 128 * 4, dtype=np.uint8), 128, 128, 4),
         ("flat640x480x4", np.tile(np.array([9, 8, 7, 255], np.uint8), 640 * 480), 640, 480, 4),
