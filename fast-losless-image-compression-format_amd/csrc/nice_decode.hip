@@ -395,15 +395,29 @@ __device__ __forceinline__ uint32_t pay_stream(uint32_t m, uint32_t i) {
 
 // One pixel event at a prefix position: the prefix and, for a coded pixel, its
 // payload symbols.  Returns the prefix; s0..s3 receive the payload.
-__device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, const LutLds& S, uint32_t gp_pfx,
-                                                uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
-  const uint32_t pfx = dsym_gp(L, my, S, PFX_STREAM, gp_pfx);
+// The frame's stream parameters (S.gp) held in scalar registers: a payload
+// symbol's parameters are selected by the prefix instead of read from LDS, so
+// its LUT lookup does not wait on a dependent LDS read.
+struct StreamParams {
+  uint32_t g[N_STREAMS];
+  __device__ __forceinline__ void load(const LutLds& S) {
+#pragma unroll
+    for (int i = 0; i < N_STREAMS; ++i) g[i] = __builtin_amdgcn_readfirstlane(S.gp[i]);
+  }
+};
+__device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, const LutLds& S,
+                                                const StreamParams& G, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                                uint32_t& s3) {
+  const uint32_t pfx = dsym_gp(L, my, S, PFX_STREAM, G.g[PFX_STREAM]);
   if (pfx < (uint32_t)P_RUN1) {
-    s0 = dsym(L, my, S, pay_stream(pfx, 0));
-    if (pfx == (uint32_t)P_RGB || pfx == (uint32_t)P_LUMA || pfx == (uint32_t)P_LUMA2) {
-      s1 = dsym(L, my, S, pay_stream(pfx, 1));
-      s2 = dsym(L, my, S, pay_stream(pfx, 2));
-      if (pfx == (uint32_t)P_LUMA) s3 = dsym(L, my, S, S_LUMA_OTHER);
+    const bool rgb = pfx == (uint32_t)P_RGB, lu = pfx == (uint32_t)P_LUMA, l2 = pfx == (uint32_t)P_LUMA2;
+    const uint32_t gp0 = pfx == (uint32_t)P_BACK_REF ? G.g[S_BACK_REF] : rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_REF]
+                       : l2 ? G.g[S_LUMA2_BASE] : G.g[S_SMALL_DIFF];
+    s0 = dsym_gp(L, my, S, pay_stream(pfx, 0), gp0);
+    if (rgb || lu || l2) {
+      s1 = dsym_gp(L, my, S, pay_stream(pfx, 1), rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_BASE] : G.g[S_LUMA2_R]);
+      s2 = dsym_gp(L, my, S, pay_stream(pfx, 2), rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_OTHER] : G.g[S_LUMA2_B]);
+      if (lu) s3 = dsym_gp(L, my, S, S_LUMA_OTHER, G.g[S_LUMA_OTHER]);
     }
   }
   return pfx;
@@ -490,7 +504,8 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
   if (jb * DEC_PARSE_THREADS + wave * 64u >= nc) return;
-  const uint32_t gp_pfx = S.gp[PFX_STREAM];
+  StreamParams SP;
+  SP.load(S);
   uint32_t* wring = ring + wave * 64u * RING_STRIDE;
   const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
   const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
@@ -535,7 +550,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
     if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
     if (active) {
       uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-      const uint32_t pfx = pixel_event(L, my, S, gp_pfx, s0, s1, s2, s3);
+      const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
       const uint32_t c = pixel_count(pfx, dk);
       px = sat_add(px, c);
       if (keep) {
@@ -777,7 +792,8 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6;
   if (vb * DEC_PARSE_THREADS + wave * 64u >= nv) return;
-  const uint32_t gp_pfx = S.gp[PFX_STREAM];
+  StreamParams SP;
+  SP.load(S);
   const uint32_t v = vb * DEC_PARSE_THREADS + threadIdx.x;
   const uint32_t item = !a.head_items ? v
                       : v < nv ? a.head_items[(uint64_t)f * a.max_chunks * subs + v] : 0u;
@@ -844,7 +860,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
     if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
     if (!active) continue;
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    const uint32_t pfx = pixel_event(L, my, S, gp_pfx, s0, s1, s2, s3);
+    const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
     if (at_n) {
       // the reference still reads one more prefix (code.rs:660): a run digit
       // there makes it copy past its buffer
