@@ -131,7 +131,7 @@ def max_over_ranks(value, dist, device):
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return value
     import torch
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device="cpu" if dist.get_backend() == "gloo" else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -170,12 +170,13 @@ def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
     rows = syn_frames(torch, 1, W, H, 11, device, y0, y1).view(-1)
     px = rows[(p0 - y0 * W) * 4:(p1 - y0 * W) * 4]
     be = S.HipBands(device.index or 0)
-    out = S.encode_sharded(be, dist, px, p0, W, H, 4)   # warmup
+    cdev = "cpu" if dist.get_backend() == "gloo" else None   # where collective tensors live
+    out = S.encode_sharded(be, dist, px, p0, W, H, 4, device=cdev)   # warmup
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        out = S.encode_sharded(be, dist, px, p0, W, H, 4)
+        out = S.encode_sharded(be, dist, px, p0, W, H, 4, device=cdev)
     torch.cuda.synchronize()
     dist.barrier()
     el = max_over_ranks((time.perf_counter() - t0) / reps, dist, device)
@@ -250,11 +251,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # tests only: NICE_DIST_BACKEND=gloo with NICE_ONE_GPU=1 runs every rank on
+    # GPU 0 (rehearses the multi-rank legs on a one-GPU box)
+    gpu = 0 if os.environ.get("NICE_ONE_GPU") == "1" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(os.environ.get("NICE_DIST_BACKEND", "nccl"))
+    device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
     nice = importlib.import_module(PKG)
     L = nice.lib()
@@ -271,7 +275,7 @@ def main():
     lens = torch.zeros(F, dtype=torch.int64, device=device)
     dec = torch.empty((F, N * 4), dtype=torch.uint8, device=device)
     status = torch.zeros(F, dtype=torch.int32, device=device)
-    ctx = nice._ctx(local)
+    ctx = nice._ctx(gpu)
 
     def step():
         nice.encode_batch(px, W, H, 4, streams, lens)
