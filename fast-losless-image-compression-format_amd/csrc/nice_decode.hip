@@ -375,9 +375,6 @@ __device__ __forceinline__ uint32_t dsym_gp(Lane& L, const uint32_t* my, const L
   L.avail += need ? 32u : 0u;
   return e >> 5;
 }
-__device__ __forceinline__ uint32_t dsym(Lane& L, const uint32_t* my, const LutLds& S, uint32_t st) {
-  return dsym_gp(L, my, S, st, S.gp[st]);
-}
 constexpr uint32_t PFX_STREAM = S_PREFIX;
 // payload stream i of mode m (code.rs:576-644), 4 bits each at 4 * (4m + i)
 constexpr unsigned long long PAY_STREAMS =
