@@ -488,9 +488,11 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
   const uint32_t r = xr + K3(256u) - pred;
   const uint32_t rec_br = P_BACK_REF | (bk << 3);
   const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
-  const uint32_t rec_l2 = P_LUMA2 | (((t2 >> 10) & 63u) << 3) | ((t2 & 31u) << 9) | (((t2 >> 20) & 31u) << 14);
-  const uint32_t rec_lu = P_LUMA | (lk << 3) | (((lt >> 10) & 63u) << 7) | ((lt & 31u) << 13) |
-                          (((lt >> 20) & 31u) << 18);
+  // LUMA2 and LUMA share the g | r << 6 | b << 11 field layout (LUMA: after its 4-bit reference)
+  const uint32_t ts = l2 ? t2 : lt;
+  const uint32_t lf = ((ts >> 10) & 63u) | ((ts & 31u) << 6) | (((ts >> 20) & 31u) << 11);
+  const uint32_t rec_l2 = P_LUMA2 | (lf << 3);
+  const uint32_t rec_lu = P_LUMA | (lk << 3) | (lf << 7);
   const uint32_t rec_rgb = P_RGB | ((r & 255u) << 3) | (((r >> 10) & 255u) << 11) | (((r >> 20) & 255u) << 19);
   return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
 }
