@@ -139,6 +139,33 @@ def test_batch_device_roundtrip(nice, O):
     assert np.array_equal(got[:, :, :3], frames.reshape(n, -1, 4)[:, :, :3])
 
 
+def test_config3_batch_64x1080p(nice, O):
+    """BASELINE config 3: a batch of 64 x 1920x1080 RGBA frames through the
+    device batch API -- every stream byte-exact to the oracle, every frame
+    decoded back."""
+    import torch
+    w, h, c, n = 1920, 1080, 4, 64
+    frames = np.stack([O.gen_syn_v1(w, h, c, s) for s in range(1, n + 1)])
+    px = torch.from_numpy(frames).cuda()
+    bound = (nice.encode_bound(w, h) + 255) // 256 * 256
+    out = torch.zeros((n, bound), dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(n, dtype=torch.int64, device="cuda")
+    nice.encode_batch(px, w, h, c, out, lens)
+    dec = torch.zeros((n, w * h * 4), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(n, dtype=torch.int32, device="cuda")
+    nice.decode_batch(out, lens, w, h, 4, dec, status)
+    torch.cuda.synchronize()
+    L = lens.cpu().numpy()
+    host = out.cpu().numpy()
+    for i in range(n):
+        want = O.encode(frames[i], w, h, c)
+        assert L[i] == len(want), i
+        assert bytes(host[i, :L[i]]) == want, i
+    assert (status.cpu().numpy() == 0).all()
+    got = dec.view(n, -1, 4)[:, :, :3]
+    assert torch.equal(got, px.view(n, -1, 4)[:, :, :3])
+
+
 @pytest.mark.parametrize("bits", [2048, 16384])
 def test_decode_long_slices(nice, O, bits, monkeypatch):
     """Long parse slices: emission runs from checkpoint sub-slices (the default
