@@ -139,6 +139,20 @@ def test_batch_device_roundtrip(nice, O):
     assert np.array_equal(got[:, :, :3], frames.reshape(n, -1, 4)[:, :, :3])
 
 
+def test_config2_single_4k(nice, O):
+    """BASELINE config 2: one 3840x2160 RGBA frame through the host entry points
+    (nice_encode / nice_decode): byte-exact stream, exact round trip."""
+    w, h, c = 3840, 2160, 4
+    px = O.gen_syn_v1(w, h, c, 2)
+    want = O.encode(px, w, h, c)
+    got = nice.encode_bytes(px.tobytes(), w, h, c)
+    assert bytes(got) == want
+    dec, img = nice.decode_bytes(want)
+    assert (img.width, img.height, img.channels) == (w, h, c)
+    g = np.frombuffer(dec, np.uint8).reshape(-1, 4)
+    assert np.array_equal(g[:, :3], px.reshape(-1, 4)[:, :3])
+
+
 def test_config3_batch_64x1080p(nice, O):
     """BASELINE config 3: a batch of 64 x 1920x1080 RGBA frames through the
     device batch API -- every stream byte-exact to the oracle, every frame
