@@ -23,7 +23,7 @@ def _sharded():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(1000, 700, 4, 2), (2048, 300, 3, 3), (640, 480, 4, 4)])
+@pytest.mark.parametrize("shape", [(1000, 700, 4, 2), (2048, 300, 3, 3), (640, 480, 4, 4), (8192, 8192, 4, 8)])
 def test_band_api_matches_oracle(nice, O, shape):
     import torch
     S = _sharded()
