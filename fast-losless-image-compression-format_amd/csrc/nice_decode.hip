@@ -771,7 +771,9 @@ struct RecGroup {
 // Lanes take sub-slices of DEC_EMIT_BITS: sub-slice s of slice j starts at the
 // converged parse's checkpoint (s * DEC_EMIT_BITS / 128 - 1) -- a prefix
 // position with its run digits and pixel count -- so emission parallelism does
-// not depend on the slice size the sync pass uses.
+// not depend on the slice size the sync pass uses.  With the first pass's
+// events kept (a.ev), the lanes take dec_heads' list instead and each stops at
+// its slice's meeting point; dec_place writes the rest.
 __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
