@@ -286,7 +286,9 @@ def main():
     torch.cuda.synchronize()
     # correctness of the measured work (outside the timed region)
     assert int(status.abs().sum()) == 0, "decode reported an error"
-    assert torch.equal(dec.view(F, N, 4)[:, :, :3], px.view(F, N, 4)[:, :, :3]), "round trip mismatch"
+    for c in range(0, F, 64):   # chunked: a whole-batch RGB slice copy does not fit beside 1024 frames
+        assert torch.equal(dec.view(F, N, 4)[c:c + 64, :, :3], px.view(F, N, 4)[c:c + 64, :, :3]), \
+            "round trip mismatch"
     stream_bytes = int(lens.sum())
 
     L.nice_ctx_set_timing(ctx.ptr, 1)
