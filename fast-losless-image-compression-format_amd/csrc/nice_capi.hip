@@ -96,7 +96,7 @@ int check_device(int device) {
 
 static const char* kPhaseNames[NICE_PHASES] = {
     "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_tilebits", "enc_tilescan",
-    "enc_pack", "enc_tail", "enc_serial", "dec_tables", "dec_sync", "dec_scan", "dec_emit",
+    "enc_pack", "enc_tail", "enc_pack_long", "dec_tables", "dec_sync", "dec_scan", "dec_emit",
     "dec_reconstruct", "dec_place"};
 
 // Optional per-phase HIP-event timing (bench / profiling).
@@ -192,6 +192,8 @@ void nice_ctx_destroy(nice_ctx* ctx) {
   ctx->host_px.release();
   ctx->host_out.release();
   ctx->dev_len.release();
+  ctx->band.release();
+  ctx->band_hdr.release();
   ctx->timer.release();
   (void)hipSetDevice(prev);
   delete ctx;
@@ -322,11 +324,14 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     ctx->timer.begin(NICE_PH_ENC_PACK, st);
     hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
     ctx->timer.end(st);
+    // frames with codes over 25 bits (FLAG_LONG; the launches return at once
+    // for the others): codes that fit the cache, then the wrapped writes
+    ctx->timer.begin(NICE_PH_ENC_LONG, st);
+    hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
+    hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);
+    ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_TAIL, st);
     hipLaunchKernelGGL(enc_tail, dim3((n_frames + 63) / 64), dim3(64), 0, st, a);
-    ctx->timer.end(st);
-    ctx->timer.begin(NICE_PH_ENC_SERIAL, st);
-    hipLaunchKernelGGL(enc_serial, dim3(n_frames), dim3(64), 0, st, a);
     ctx->timer.end(st);
   }
   NICE_HIP(hipGetLastError());
@@ -738,12 +743,8 @@ int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, 
   unsigned long long* info = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
   hipLaunchKernelGGL(enc_band_sum, dim3(1), dim3(256), 0, st, a, info);
   unsigned long long hinfo[2];
-  uint32_t flags = 0;
   NICE_HIP(hipMemcpyAsync(hinfo, info, 16, hipMemcpyDeviceToHost, st));
-  NICE_HIP(hipMemcpyAsync(&flags, a.frame_flags, 4, hipMemcpyDeviceToHost, st));
   NICE_HIP(hipStreamSynchronize(st));
-  // codes longer than 25 bits need the serial writer over the whole image
-  if (flags & FLAG_SERIAL) return NICE_E_UNSUPPORTED;
   ctx->bs.band_bits = hinfo[0];
   ctx->bs.seed_bit = hinfo[1];
   ctx->bs.tabled = true;
@@ -769,8 +770,11 @@ int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_
   a.band_bit0 = band_bit0;
   a.out = (uint8_t*)d_words - (int64_t)(band_bit0 >> 5) * 4;   // virtual: stream word w at d_words[w - w0]
   a.out_stride = 0;
+  const uint32_t tblocks = std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u);
   hipLaunchKernelGGL(enc_tilescan, dim3(1), dim3(1024), 0, st, a);
-  hipLaunchKernelGGL(enc_pack, dim3(std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
+  hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }

@@ -17,9 +17,11 @@
 //                  32 bits so every output word is written once, no zero-fill,
 //                  no global atomics), MSB-first packing (bitwriter.rs:55-73) and
 //                  the tail (hfe.rs:115, code.rs:421-422).
-//   enc_serial     exact single-lane replay of the reference writer, used only
-//                  for frames whose emitted codes exceed FAST_MAX_CODE_BITS
-//                  (where the reference's u32 cache arithmetic mangles bits).
+//   enc_pack_long  frames whose emitted codes exceed FAST_MAX_CODE_BITS: the
+//                  same tile-parallel placement with full-length codes, then
+//                  the writes that wrap the reference's u32 cache (pending +
+//                  length > 32, bitwriter.rs:63-64) applied to their 32-bit
+//                  windows in a second pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -779,7 +781,7 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
       prev = aob;
     }
     a.stream_max[(uint64_t)f * N_STREAMS + s] = (uint8_t)my_max;
-    if (my_emit_max > FAST_MAX_CODE_BITS) atomicOr(&a.frame_flags[f], FLAG_SERIAL);
+    if (my_emit_max > FAST_MAX_CODE_BITS) atomicOr(&a.frame_flags[f], FLAG_LONG);
   }
 }
 
@@ -834,9 +836,8 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
   bool normal = true;
   for (int s = 0; s < N_STREAMS; ++s) normal &= smax[s] <= 31;
   const uint64_t N = (uint64_t)a.W * a.H;
-  const bool serial_frame = (a.frame_flags[f] & FLAG_SERIAL) != 0;
 
-  if (normal && !serial_frame && N > 0) {
+  if (normal && N > 0) {
     // Every field sits at a fixed bit offset: assemble 32-bit MSB-first words.
     for (int w = lane; w < 200; w += 64) words[w] = 0;
     __syncthreads();
@@ -883,7 +884,7 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
     return;
   }
   if (lane != 0) return;
-  // Serial exact path (spilled 5-bit fields, 8-bit fields, serial frames, empty frames).
+  // Serial exact path (spilled 5-bit fields, 8-bit fields, empty frames).
   for (int k = 0; k < 4; ++k) out[k] = "nice"[k];
   for (int k = 0; k < 4; ++k) out[4 + k] = (uint8_t)(a.W >> (24 - 8 * k));
   for (int k = 0; k < 4; ++k) out[8 + k] = (uint8_t)(a.H >> (24 - 8 * k));
@@ -907,14 +908,14 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
   uint32_t suf = (uint32_t)acc;
   if (bw.bit_offset) suf = (suf << bw.bit_offset) | (bw.cache >> (32 - bw.bit_offset));
   a.seed_suf[f] = suf;
-  if (!serial_frame && N > 0) {
+  if (N > 0) {
     // pending bits (top bit_offset bits of the cache), then zeros to the end of
     // the word holding the data start: the first data tile ORs into it
     const uint64_t wend = ((pos >> 5) + 1) * 4;
     out[bw.pos] = bw.bit_offset ? (uint8_t)((bw.cache >> 24) & (0xFFu << (8 - bw.bit_offset))) : 0u;
     for (uint64_t q = bw.pos + 1; q < wend; ++q) out[q] = 0;
   }
-  if (N == 0 && !serial_frame) {
+  if (N == 0) {
     // no data symbols: tail only (hfe.rs:115, code.rs:421-422)
     const uint8_t P = (uint8_t)(bw.cache >> 24);
     uint64_t p = bw.pos;
@@ -1017,6 +1018,40 @@ __device__ __forceinline__ void quad_bits(const uint32_t* tbl, const RecBinTable
 __device__ __forceinline__ void load_tbl(uint32_t* tbl, const EncArgs& a, uint32_t f) {
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
 }
+__device__ __forceinline__ void load_lens(uint32_t* lens, const EncArgs& a, uint32_t f) {
+  for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) lens[b] = a.tbl_len8[(uint64_t)f * N_BINS + b];
+}
+
+// Bits of the thread's 4 pixels (prefix, payload, run digits) from full code
+// lengths (any length: also the frames with codes over FAST_MAX_CODE_BITS).
+__device__ __forceinline__ uint32_t quad_nbits(const uint32_t* lens, const RecBinTable& rbt, const uint32_t* mask,
+                                               int64_t start, int count, int p0, uint32_t next_tile_px,
+                                               const TileQuad& Q) {
+  const int nx_local = next_coded_local(mask, p0 + 3);
+  const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)next_tile_px;
+  uint32_t nb = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!((Q.nib >> q) & 1u)) continue;
+    uint32_t b0, b1, b2, b3;
+    const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
+    nb += lens[BIN_PREFIX + min(Q.rc[q] & 7u, 4u)] + lens[b0];
+    if (n > 1) nb += lens[b1] + lens[b2];
+    if (n > 3) nb += lens[b3];
+    const uint32_t later = Q.nib >> (q + 1);
+    const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
+    const uint64_t run = nxt - (uint64_t)(start + p0 + q) - 1;
+    if (run > 0) {
+      uint64_t m = run - 1;
+      while (true) {
+        nb += lens[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
+        if (m < 8) break;
+        m >>= 3;
+      }
+    }
+  }
+  return nb;
+}
 
 // Contiguous tile ranges per block (the code table is reloaded only when the
 // frame changes); records are fetched one tile ahead.
@@ -1049,16 +1084,14 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
     nx.step(1);
     if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
     const uint32_t f = it.f, tt = it.tt();
-    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // block-uniform
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
     __syncthreads();
-    if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
+    if (f != cur_f) { load_lens(tbl, a, f); cur_f = f; }
     TileQuad Q;
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
-    quad_bits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
-    uint32_t x = Q.nb;
+    uint32_t x = quad_nbits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
     if (lane == 0) wsum[wid] = x;
@@ -1083,11 +1116,10 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
   for (uint64_t w = t0 + wid; w < t1; w += 4, it.step(4)) {
     const uint64_t t = it.tile();
     const uint32_t f = it.f;
-    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // wave-uniform
     if (f != cur_f) {
       __builtin_amdgcn_wave_barrier();
       for (int b = lane; b < (int)(2 * TH_WORDS); b += 64)
-        lens[b] = b < N_BINS ? (a.tbl[(uint64_t)f * N_BINS + b] & 31u) : 0u;
+        lens[b] = b < N_BINS ? (uint32_t)a.tbl_len8[(uint64_t)f * N_BINS + b] : 0u;
       cur_f = f;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
@@ -1127,7 +1159,6 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
 __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   __shared__ unsigned long long part[1024];
   const uint32_t f = blockIdx.x;
-  if (a.frame_flags[f] & FLAG_SERIAL) return;
   const uint32_t nt = a.tile_hi - a.tile_lo;
   const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo;
   const uint32_t per = (nt + 1023) / 1024;
@@ -1187,7 +1218,7 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
     nx.step(1);
     if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
     const uint32_t f = it.f, tt = it.tt();
-    if (a.frame_flags[f] & FLAG_SERIAL) continue;   // enc_serial's frame
+    if (a.frame_flags[f] & FLAG_LONG) continue;   // enc_pack_long's frame (block-uniform)
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
     __syncthreads();
@@ -1288,7 +1319,7 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
 __global__ __launch_bounds__(64) void enc_tail(EncArgs a) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
   if (f >= a.n_frames) return;
-  if ((a.frame_flags[f] & FLAG_SERIAL) || (uint64_t)a.W * a.H == 0) return;
+  if ((uint64_t)a.W * a.H == 0) return;
   uint8_t* out = a.out + (uint64_t)f * a.out_stride;
   const uint64_t e0 = a.data_end[f];
   const uint64_t B = e0 >> 3;            // the partial byte (the reference's cache >> 24)
@@ -1302,62 +1333,136 @@ __global__ __launch_bounds__(64) void enc_tail(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K6: exact serial replay for flagged frames (emitted code > 25 bits).
+// K6: frames with codes over FAST_MAX_CODE_BITS (FLAG_LONG).
+//
+// A write of an n-bit code at absolute stream bit p behaves like the
+// reference's write_24bits (bitwriter.rs:55-73) with bit_offset = p & 7
+// (the writer flushes every whole byte, so bit_offset is always the position
+// mod 8 once the table header is out):
+//  * (p & 7) + n <= 32: the code lands exactly on bits [p, p + n);
+//  * otherwise `32 - bit_offset` wraps (u8) and the shift is masked to 5 bits:
+//    the 32-bit window at byte p >> 3 becomes window + (code << ((32 - (p & 7)
+//    - n) & 31)) mod 2^32 -- carries into the pending bits of the codes before
+//    it included -- and every bit after the window up to p + n is zero (the
+//    flush loop shifts the cache out).
+// Phase 0 places the codes of the first kind (global atomicOr after the tile
+// zeroes the words only it writes; enc_tilescan zeroed the shared ones).
+// Phase 1 re-derives every symbol's position and applies the wrapped writes to
+// their windows, whose earlier bits phase 0 has finalised.  Wrapped windows
+// are disjoint: a window ends before its code's end (p + n > window + 32),
+// and the next code starts there.  In band mode a window never reaches into
+// the previous band: a band's first code is the prefix code of its first coded
+// pixel (stream SC_PREFIXES, 13 symbols: at most 12 bits), never a long one.
 // ---------------------------------------------------------------------------
-struct GlobalAcc {
-  const uint8_t* frame;
-  int C;
-  uint32_t W;
-  int64_t i;
-  __device__ __forceinline__ uint32_t operator()(int rows, int px) const {
-    const int64_t j = i - ((int64_t)rows * W + px);
-    return load_spread(frame, j, C);
-  }
-};
+__device__ __forceinline__ void wrapped_write(uint8_t* out, uint64_t p, uint32_t v, uint32_t n) {
+  const uint64_t B = p >> 3;
+  const uint32_t bo = (uint32_t)(p & 7u);
+  const uint32_t sh = (uint32_t)(uint8_t)(32u - (uint8_t)(bo + n)) & 31u;
+  const uint32_t w = ((uint32_t)out[B] << 24) | ((uint32_t)out[B + 1] << 16) | ((uint32_t)out[B + 2] << 8) | out[B + 3];
+  const uint32_t r = w + (v << sh);
+  out[B] = (uint8_t)(r >> 24);
+  out[B + 1] = (uint8_t)(r >> 16);
+  out[B + 2] = (uint8_t)(r >> 8);
+  out[B + 3] = (uint8_t)r;
+}
 
-__global__ __launch_bounds__(64) void enc_serial(EncArgs a) {
-  const uint32_t f = blockIdx.x;
-  if (!(a.frame_flags[f] & FLAG_SERIAL)) return;
-  if (threadIdx.x != 0) return;
-  const uint8_t* frame = a.px + (uint64_t)f * a.frame_stride;
-  uint8_t* out = a.out + (uint64_t)f * a.out_stride;
-  const uint64_t N = (uint64_t)a.W * a.H;
-  DevBitwriter bw{out, a.hdr_bytes[f], a.hdr_bitoff[f], a.hdr_cache[f]};
-  const uint64_t fb = (uint64_t)f * N_BINS;
-  auto emit = [&](uint32_t bin) {
-    // write_24bits(aob, code as u32) with the full u8 length and usize code
-    const uint8_t aob = a.tbl_len8[fb + bin];
-    bw.write_24bits(aob, a.tbl_code[fb + bin]);
-  };
-  uint64_t i = 0;
-  while (i < N) {
-    PixSyms s;
-    GlobalAcc acc{frame, (int)a.C, a.W, (int64_t)i};
-    classify<false>((uint32_t)i, a.W, acc, s);
-    emit(BIN_PREFIX + s.mode);
+__global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phase) {
+  __shared__ uint32_t code[N_BINS];
+  __shared__ uint32_t lens[N_BINS];
+  __shared__ uint32_t mask[ENC_TILE / 32];
+  __shared__ uint32_t wsum[ENC_THREADS / 64];
+  __shared__ RecBinTable rbt;
+  rbt_init(rbt, threadIdx.x);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t N = (int64_t)a.W * a.H;
+  const int p0 = 4 * threadIdx.x;
+  uint32_t cur_f = NONE;
+  uint64_t t0, t1;
+  tile_range(a, t0, t1);
+  TileIter it(a, t0);
+  for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
+    const uint32_t f = it.f, tt = it.tt();
+    if (!(a.frame_flags[f] & FLAG_LONG)) continue;   // block-uniform
+    const uint64_t t = it.tile();
+    const int64_t start = (int64_t)tt * ENC_TILE;
+    const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+    uint32_t rc[4];
+    quad_fetch(a, f, tt, p0, rc);
+    __syncthreads();
+    if (f != cur_f) {
+      for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) {
+        code[b] = a.tbl_code[(uint64_t)f * N_BINS + b];
+        lens[b] = a.tbl_len8[(uint64_t)f * N_BINS + b];
+      }
+      cur_f = f;
+    }
+    TileQuad Q;
+    quad_mask(rc, lane, wid, mask, Q);
+    __syncthreads();
+    const uint32_t nb = quad_nbits(lens, rbt, mask, start, count, p0, a.tile_next[t], Q);
+    const uint32_t x = wave_incl_scan(nb);
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tile_bits = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((uint32_t)k < s.n) emit(s.b[k]);
-    const uint32_t X = acc(0, 0);
-    uint64_t j = i + 1;
-    while (j < N && load_spread(frame, (int64_t)j, a.C) == X) ++j;
-    const uint64_t run = j - i - 1;
-    if (run > 0) {
-      uint64_t m = run - 1;
-      while (true) {
-        emit(BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u));
-        if (m < 8) break;
-        m >>= 3;
+    for (int k = 0; k < ENC_THREADS / 64; ++k) {
+      const uint32_t ws = wsum[k];
+      wbase += (k < wid) ? ws : 0u;
+      tile_bits += ws;
+    }
+    const uint64_t s0 = a.tile_off[t];
+    uint8_t* out = a.out + (uint64_t)f * a.out_stride;
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
+    if (phase == 0) {
+      const uint64_t e0 = s0 + tile_bits, w0 = s0 >> 5;
+      const uint32_t nw = tile_bits ? (uint32_t)(((e0 + 31) >> 5) - w0) : 0u;
+      for (uint32_t m = threadIdx.x; m < nw; m += ENC_THREADS) {
+        const bool shared = (m == 0 && (s0 & 31)) || (m == nw - 1 && (e0 & 31));
+        if (!shared) out32[w0 + m] = 0u;
+      }
+      __threadfence();
+      __syncthreads();
+    }
+    uint64_t pos = s0 + wbase + x - nb;
+    auto emit = [&](uint32_t bin) {
+      const uint32_t n = lens[bin], v = code[bin];
+      const uint32_t bo = (uint32_t)(pos & 7u);
+      if (bo + n <= 32u) {
+        if (phase == 0 && n) {
+          const uint32_t o = (uint32_t)(pos & 31u);
+          const uint64_t y = (uint64_t)v << (64u - o - n);
+          atomicOr(&out32[pos >> 5], __builtin_bswap32((uint32_t)(y >> 32)));
+          if (o + n > 32u) atomicOr(&out32[(pos >> 5) + 1], __builtin_bswap32((uint32_t)y));
+        }
+      } else if (phase == 1 && !(a.band && (pos & ~7ull) < a.band_bit0)) {
+        wrapped_write(out, pos, v, n);
+      }
+      pos += n;
+    };
+    const int nx_local = next_coded_local(mask, p0 + 3);
+    const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)a.tile_next[t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!((Q.nib >> q) & 1u)) continue;
+      uint32_t b0, b1, b2, b3;
+      const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
+      emit(BIN_PREFIX + min(Q.rc[q] & 7u, 4u));
+      emit(b0);
+      if (n > 1) { emit(b1); emit(b2); }
+      if (n > 3) emit(b3);
+      const uint32_t later = Q.nib >> (q + 1);
+      const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
+      const uint64_t run = nxt - (uint64_t)(start + p0 + q) - 1;
+      if (run > 0) {
+        uint64_t m = run - 1;
+        while (true) {
+          emit(BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u));
+          if (m < 8) break;
+          m >>= 3;
+        }
       }
     }
-    i = j;
   }
-  out[bw.pos] = (uint8_t)(bw.cache >> 24);
-  out[bw.pos + 1] = (uint8_t)(bw.cache >> 24);
-  out[bw.pos + 2] = (uint8_t)(bw.cache >> 16);
-  out[bw.pos + 3] = (uint8_t)(bw.cache >> 8);
-  out[bw.pos + 4] = (uint8_t)(bw.cache);
-  a.out_len[f] = bw.pos + 5;
 }
 
 }  // namespace nice

@@ -7,7 +7,9 @@
 namespace nice {
 
 constexpr int ENC_TILE = 1024;          // pixels per encoder tile (raster-contiguous)
-constexpr uint32_t FLAG_SERIAL = 1u;    // frame needs the exact serial writer
+// frame emits a code longer than FAST_MAX_CODE_BITS: packed by enc_pack_long
+// (the reference writer's u32 cache wraps for such codes, bitwriter.rs:63-64)
+constexpr uint32_t FLAG_LONG = 1u;
 
 struct EncArgs {
   // input: n_frames frames of W*H pixels, C bytes per pixel, frame_stride bytes apart
@@ -72,7 +74,10 @@ __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
 __global__ void enc_band_sum(EncArgs a, unsigned long long* info);
 __global__ void enc_band_merge(uint32_t* out32, const uint32_t* words, const unsigned long long* band_w0,
                                const unsigned long long* band_off, uint32_t R);
-__global__ void enc_serial(EncArgs a);
+// long-code frames (FLAG_LONG): phase 0 packs every code whose write does not
+// wrap the reference cache (pending + length <= 32); phase 1 applies the
+// wrapped writes to their 32-bit windows once phase 0's bits are final
+__global__ void enc_pack_long(EncArgs a, int phase);
 
 }  // namespace nice
 

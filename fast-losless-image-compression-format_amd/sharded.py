@@ -12,8 +12,14 @@ the CPU tests):
 2. all-reduce of the 858-bin symbol histogram, so every rank builds the same
    Huffman tables (hfe.rs:51-117);
 3. all-gather of the band bit counts: each band's bit offset in the stream;
-4. gather-v of the band words to the root (point-to-point sends), which ORs
-   the shared boundary words and writes header and tail.
+4. gather-v of the band words to the root (grouped point-to-point sends and
+   receives, ``batch_isend_irecv`` = one ncclGroupStart/End on RCCL, so the
+   peers' transfers run concurrently over their own xGMI links), which ORs the
+   shared boundary words and writes header and tail.
+
+A band step that fails on one rank (a NiceError from the C ABI) is reported
+through the next exchange (an error word rides along in each gathered or
+reduced tensor), so every rank raises instead of waiting in a collective.
 
 The root's bytes equal ``encode_bytes`` of the whole image.  The band steps
 go through a *backend* object (``HipBands`` drives libnice_hip.so); the
@@ -91,8 +97,10 @@ class HipBands:
         return hist
 
     def tables(self, hist_total):
+        import torch
         bits, seed = ctypes.c_uint64(), ctypes.c_uint64()
-        h = hist_total.to(dtype=hist_total.dtype).contiguous()
+        # the C ABI reads the histogram on this rank's GPU (gloo reduces on the host)
+        h = hist_total.to(device=f"cuda:{self.device}", dtype=torch.int32).contiguous()
         self._check(self.L.nice_band_tables(self.ctx.ptr, self._st(), ctypes.c_void_p(h.data_ptr()),
                                             ctypes.byref(bits), ctypes.byref(seed)), "nice_band_tables")
         return int(bits.value), int(seed.value)
@@ -124,6 +132,21 @@ class HipBands:
         return out[: n.value]
 
 
+def _step(fn, *args):
+    """Runs a band step; returns (result, 0) or (None, status code)."""
+    from . import NiceError
+    try:
+        return fn(*args), 0
+    except NiceError as e:
+        return None, int(e.code) if int(e.code) else -1
+
+
+def _raise_if(err: int, what: str):
+    if err:
+        from . import NiceError
+        raise NiceError(err, what + " (on some rank)")
+
+
 def encode_sharded(backend, dist, px, px0: int, width: int, height: int, channels: int,
                    channels_out: int | None = None, root: int = 0, device=None):
     """Encode one image across the ranks of the default process group.
@@ -138,36 +161,54 @@ def encode_sharded(backend, dist, px, px0: int, width: int, height: int, channel
     co = channels if channels_out is None else channels_out
     n = width * height
     lo, hi = band_tiles(width, height, rank, world)
-    # 1. edges -> the first coded pixel after this band
-    edges = backend.classify(px, px0, width, height, channels, co, lo, hi).to(dev)
-    all_edges = [torch.empty_like(edges) for _ in range(world)]
-    dist.all_gather(all_edges, edges)
-    later = [int(e[0]) for e in all_edges[rank + 1:] if int(e[0]) != NONE]
+    # 1. edges -> the first coded pixel after this band (+ error word)
+    edges, err = _step(backend.classify, px, px0, width, height, channels, co, lo, hi)
+    if edges is None:
+        edges = torch.full((2,), NONE, dtype=torch.int64)
+    mine = torch.cat([edges.to(device=dev, dtype=torch.int64),
+                      torch.tensor([err], dtype=torch.int64, device=dev)])
+    all_edges = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(all_edges, mine)
+    ge = torch.stack(all_edges).cpu()
+    _raise_if(int(ge[:, 2].min()), "nice_band_classify")
+    later = [int(e[0]) for e in ge[rank + 1:] if int(e[0]) != NONE]
     band_next = later[0] if later else n
-    # 2. histogram -> identical tables everywhere
-    hist = backend.runs(band_next).to(dev)
-    dist.all_reduce(hist)
-    bits, seed = backend.tables(hist)
+    # 2. histogram -> identical tables everywhere (error count in the last slot)
+    hist, err = _step(backend.runs, band_next)
+    h = torch.zeros(859, dtype=torch.int64, device=dev)
+    if hist is not None:
+        h[:858] = hist.to(device=dev, dtype=torch.int64)
+    h[858] = 1 if err else 0
+    dist.all_reduce(h)
+    _raise_if(-1 if int(h[858]) else 0, "nice_band_runs")
+    res, err = _step(backend.tables, h[:858])
+    bits, seed = res if res is not None else (0, 0)
     # 3. bit counts -> offsets
-    b = torch.tensor([bits], dtype=torch.int64, device=dev)
+    b = torch.tensor([bits, err], dtype=torch.int64, device=dev)
     all_bits = [torch.empty_like(b) for _ in range(world)]
     dist.all_gather(all_bits, b)
-    bitss = [int(x) for x in all_bits]
+    gb = torch.stack(all_bits).cpu()
+    _raise_if(int(gb[:, 1].min()), "nice_band_tables")
+    bitss = [int(x) for x in gb[:, 0]]
     bit0s = [seed + sum(bitss[:r]) for r in range(world)]
     words = backend.pack(bit0s[rank], bitss[rank])
-    # 4. gather-v of the band words to the root
+    # 4. gather-v of the band words to the root: grouped P2P, all peers at once
     counts = [backend.words(bit0s[r], bitss[r]) for r in range(world)]
     if rank != root:
         if counts[rank]:
-            dist.send(words.to(dev).contiguous(), dst=root)
+            for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, words.to(dev).contiguous(), root)]):
+                q.wait()
         return None
-    parts = []
+    parts, ops = [], []
     for r in range(world):
         if r == rank:
             parts.append(words.to(dev))
         elif counts[r]:
             buf = torch.empty(counts[r], dtype=words.dtype, device=dev)
-            dist.recv(buf, src=r)
+            ops.append(dist.P2POp(dist.irecv, buf, r))
             parts.append(buf)
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
     cat = torch.cat(parts) if parts else words.new_zeros(0)
     return backend.assemble(cat.to(words.device), bit0s, bitss, width, height)

@@ -109,9 +109,8 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
  *      nice_band_pack       nice_band_words() words: the band's bits at their
  *                           stream position (first/last word partial)
  *   5. gather words         nice_band_assemble (one rank): header + bands + tail
- * The result equals nice_encode of the whole image byte for byte.  Frames whose
- * codes exceed 25 bits need the serial writer: nice_band_tables returns
- * NICE_E_UNSUPPORTED for them.
+ * The result equals nice_encode of the whole image byte for byte, codes longer
+ * than 25 bits included.
  * d_px holds pixels [px0, px0 + px_count) (global raster index), which must
  * cover the band and the 3 rows + 3 pixels before it. */
 int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t px0, uint64_t px_count,
@@ -159,7 +158,7 @@ int nice_png_unfilter(const uint8_t* raw, uint32_t w, uint32_t h, uint32_t bpp, 
 /* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
 enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,
-  NICE_PH_ENC_TILEBITS, NICE_PH_ENC_TILESCAN, NICE_PH_ENC_PACK, NICE_PH_ENC_TAIL, NICE_PH_ENC_SERIAL,
+  NICE_PH_ENC_TILEBITS, NICE_PH_ENC_TILESCAN, NICE_PH_ENC_PACK, NICE_PH_ENC_TAIL, NICE_PH_ENC_LONG,
   NICE_PH_DEC_TABLES, NICE_PH_DEC_SYNC, NICE_PH_DEC_SCAN, NICE_PH_DEC_EMIT, NICE_PH_DEC_RECON,
   NICE_PH_DEC_PLACE, NICE_PHASES
 };

@@ -448,9 +448,14 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
     }
     size_t header_bytes = sink.len;
     uint8_t max_emit = 0;
+    uint64_t n_long = 0, n_wrapped = 0;
     for (size_t k = 0; k < e.len; ++k) {                                /* hfe.rs:110-113 */
         int s = e.v[k].stream, sym = e.v[k].sym;
         if (aob[s][sym] > max_emit) max_emit = aob[s][sym];
+        /* diagnostics: codes over 25 bits, and writes whose u8 `32 - bit_offset`
+         * wraps (bitwriter.rs:63-64: pending + length > 32 mangles the cache) */
+        n_long += aob[s][sym] > 25;
+        n_wrapped += (unsigned)bw.bit_offset + aob[s][sym] > 32u;
         bw_write_24bits(&bw, aob[s][sym], (uint32_t)code[s][sym]);
     }
     sink_put(&sink, (uint8_t)(bw.cache >> 24));                           /* hfe.rs:115 */
@@ -463,6 +468,8 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
         stats->n_run_pixels = n_runpx;
         stats->header_end = header_bytes;
         stats->max_emitted_aob = max_emit;
+        stats->n_long_emits = n_long;
+        stats->n_wrapped_emits = n_wrapped;
         int bin = 0;
         for (int s = 0; s < N_STREAMS; ++s)
             for (int i = 0; i < STREAM_N[s]; ++i, ++bin) {
@@ -957,4 +964,71 @@ void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C) {
             p[2] = (uint8_t)((W + H > 2) ? (255u * (x + y)) / (W + H - 2) : 0);
             if (C == 4) p[3] = 255;
         }
+}
+
+/* A frame whose small-diff symbol counts grow like Fibonacci numbers, so the
+ * Huffman merge of hfe.rs:72-84 chains them: the rarest emitted symbols get
+ * codes of K-1 bits or more (over 25 bits for K >= 28).  Test input for the
+ * long-code writer path (bitwriter.rs:55-73 with bit_offset + length > 32).
+ * Pixels are generated in raster order as pred + delta (code.rs:208-247:
+ * pred = floor((U+L)/2) from row 1 on, L in row 0) with delta one of K fixed
+ * small diffs drawn with weights F(k+2); a draw is rejected when it would
+ * make the pixel a run member or a back reference (code.rs:191-206, 371-407)
+ * or leave 0..255; pixels with no valid draw take a large jump (RGB / luma). */
+void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K) {
+    if (K > 40) K = 40;
+    if (K < 2) K = 2;
+    int dl[40][3];
+    uint64_t left[40], total = 0;
+    uint64_t fa = 1, fb = 2;   /* F(2), F(3) */
+    uint32_t s = seed ? seed : 1u;
+#define XS() (s ^= s << 13, s ^= s >> 17, s ^= s << 5, s)
+    for (uint32_t k = 0; k < K; ++k) {
+        /* distinct nonzero deltas, alternating in sign by rank */
+        int c = (int)k + 1, sg = (k & 1) ? -1 : 1;
+        dl[k][0] = sg * (1 + (c % 3));
+        dl[k][1] = sg * ((c / 3) % 4);
+        dl[k][2] = -sg * ((c / 12) % 4);
+        left[k] = fa;
+        total += fa;
+        uint64_t t = fa + fb; fa = fb; fb = t;
+    }
+    const size_t N = (size_t)W * H;
+    for (size_t i = 0; i < N; ++i) {
+        uint8_t *p = px + i * C;
+        if (C == 4) p[3] = 255;
+        if (i == 0) { p[0] = 128; p[1] = 128; p[2] = 128; continue; }
+        int pred[3];
+        const uint8_t *L = px + (i - 1) * C;
+        for (int c = 0; c < 3; ++c)
+            pred[c] = i >= W ? ((int)px[(i - W) * C + c] + (int)L[c]) / 2 : (int)L[c];
+        int ok = 0;
+        for (int tries = 0; tries < 48 && !ok && total; ++tries) {
+            uint64_t r = ((uint64_t)XS() << 32 | XS()) % total;
+            uint32_t k = 0;
+            while (r >= left[k]) { r -= left[k]; ++k; }
+            int v[3], good = 1;
+            for (int c = 0; c < 3; ++c) {
+                v[c] = pred[c] + dl[k][c];
+                if (v[c] < 0 || v[c] > 255) good = 0;
+                /* drift back toward mid-range */
+                if ((pred[c] > 215 && dl[k][c] > 0) || (pred[c] < 40 && dl[k][c] < 0)) good = 0;
+            }
+            if (!good) continue;
+            for (int c = 0; c < 3; ++c) p[c] = (uint8_t)v[c];
+            /* coded (not a run member) and no back reference k = 1..4 */
+            const size_t q = i * C;
+            if (rgb_eq(px, q, q - C)) continue;
+            if (i >= W && rgb_eq(px, q, q - (size_t)W * C)) continue;
+            if (i >= W - 1 && W >= 1 && rgb_eq(px, q, q - (size_t)(W - 1) * C)) continue;
+            if (i >= 2 && rgb_eq(px, q, q - 2 * (size_t)C)) continue;
+            if (i >= 2 * (size_t)W && rgb_eq(px, q, q - 2 * (size_t)W * C)) continue;
+            ok = 1;
+            left[k] -= 1;
+            total -= 1;
+        }
+        if (!ok)
+            for (int c = 0; c < 3; ++c) p[c] = (uint8_t)(pred[c] + 64 + 37 * c + (XS() & 15));
+    }
+#undef XS
 }

@@ -31,6 +31,8 @@ typedef struct {
     uint64_t hist_total;
     uint64_t hist[858];        /* symbol counts, streams concatenated in id order */
     uint8_t aob[858];          /* code lengths, same layout */
+    uint64_t n_long_emits;     /* emitted codes longer than 25 bits */
+    uint64_t n_wrapped_emits;  /* writes with pending bits + length > 32 (bitwriter.rs:63-64 wrap) */
 } nice_oracle_stats;
 
 int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
@@ -50,6 +52,7 @@ int nice_oracle_kat_hfe(size_t *stream_len, uint8_t *max_aob);
 
 void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed);
 void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C);
+void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,8 @@ class Stats(ctypes.Structure):
         ("hist_total", ctypes.c_uint64),
         ("hist", ctypes.c_uint64 * 858),
         ("aob", ctypes.c_uint8 * 858),
+        ("n_long_emits", ctypes.c_uint64),
+        ("n_wrapped_emits", ctypes.c_uint64),
     ]
 
 
@@ -84,6 +86,8 @@ def lib():
                                              ctypes.c_uint32, ctypes.c_uint32]
         L.nice_oracle_gen_gradient.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32,
                                                ctypes.c_uint32]
+        L.nice_oracle_gen_deep_codes.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -157,6 +161,14 @@ def gen_syn_v1(width: int, height: int, channels: int, seed: int) -> np.ndarray:
 def gen_gradient(width: int, height: int, channels: int) -> np.ndarray:
     px = np.zeros(width * height * channels, dtype=np.uint8)
     lib().nice_oracle_gen_gradient(_u8p(px), width, height, channels)
+    return px
+
+
+def gen_deep_codes(width: int, height: int, channels: int, seed: int = 1, k: int = 32) -> np.ndarray:
+    """Small-diff frame with Fibonacci-skewed symbol counts: emitted codes of
+    up to about k-1 bits (test input for the long-code writer path)."""
+    px = np.zeros(width * height * channels, dtype=np.uint8)
+    lib().nice_oracle_gen_deep_codes(_u8p(px), width, height, channels, seed, k)
     return px
 
 

@@ -88,8 +88,15 @@ def test_decode_matches(nice, O, case):
     assert np.array_equal(g[:, :3].reshape(-1), rgb), name
     if c == 4:
         assert (g[:, 3] == 255).all()
-    ref, _ = O.decode(s, O.DEC_STRIDE)
-    assert np.array_equal(np.frombuffer(got, np.uint8), ref.reshape(-1, c).reshape(-1)[:len(got)]) or c == 4
+    if c == 3:
+        ref, _ = O.decode(s, O.DEC_STRIDE)
+        assert np.array_equal(np.frombuffer(got, np.uint8), ref)
+    else:
+        # RGBA: the stream is the RGB stream with header byte 12 = 4;
+        # the oracle decodes the byte-12-patched stream, alpha is filled
+        ref, dims = O.decode(s[:12] + bytes([3]) + s[13:], O.DEC_STRIDE)
+        assert dims == (w, h, 3)
+        assert np.array_equal(g[:, :3].reshape(-1), ref)
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c[4] == 3], ids=[c[0] for c in CASES if c[4] == 3])
@@ -108,11 +115,15 @@ def test_decode_strict_reference(nice, O, case):
         ok = True
     except nice.NiceError:
         ok = False
-    if ref_ok and ok:
-        assert np.array_equal(np.frombuffer(got, np.uint8), ref)
+    _, st = O.encode(px, w, h, c, with_stats=True)
+    if ref_ok and max(st.max_aob) > 24:
+        # the one deliberate conservative refusal: a table longer than 24 bits
+        # (the reference's u8 bit offset may wrap on it, bitreader.rs:88-97)
+        assert not ok, name
     else:
-        # strict mode is conservative on max length > 24; never accepts what the reference rejects
-        assert not ok or ref_ok
+        assert ok == ref_ok, (name, ok, ref_ok)
+    if ok:
+        assert np.array_equal(np.frombuffer(got, np.uint8), ref)
 
 
 def test_batch_device_roundtrip(nice, O):
@@ -239,3 +250,27 @@ def test_decode_single_wave_rows(nice, O, monkeypatch):
         got, _ = nice.decode_bytes(s)
         g = np.frombuffer(got, np.uint8).reshape(-1, c)
         assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), name
+
+
+# SYN-v1 RGB frames inside the literal reference decoder's domain (the oracle's
+# reference-mode decode terminates); (256, 64, 8) has a 25-bit table, which
+# strict mode refuses on purpose although the reference decodes it.
+STRICT_DOMAIN = [(512, 512, 1), (512, 512, 2), (333, 211, 3), (640, 480, 4), (1920, 1080, 5),
+                 (1000, 997, 6), (300, 300, 7), (256, 64, 8), (1024, 768, 9), (200, 150, 10)]
+
+
+@pytest.mark.parametrize("case", STRICT_DOMAIN, ids=[f"{w}x{h}s{s}" for w, h, s in STRICT_DOMAIN])
+def test_decode_strict_reference_domain(nice, O, case):
+    """Strict mode must decode every stream the literal reference decodes
+    (identical pixels), except the documented refusal of tables over 24 bits."""
+    w, h, seed = case
+    px = O.gen_syn_v1(w, h, 3, seed)
+    s, st = O.encode(px, w, h, 3, with_stats=True)
+    ref, _ = O.decode(s)
+    if max(st.max_aob) > 24:
+        with pytest.raises(nice.NiceError):
+            nice.decode_bytes(s, flags=nice.DEC_STRICT_REFERENCE)
+        return
+    got, _ = nice.decode_bytes(s, flags=nice.DEC_STRICT_REFERENCE)
+    assert np.array_equal(np.frombuffer(got, np.uint8), ref)
+    assert np.array_equal(ref, px)
