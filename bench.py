@@ -29,43 +29,47 @@ HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
 AMP = [0, 1, 2, 3, 8, 24, 64, 256]
 
 
-def syn_frames(torch, n, W, H, seed0, device, y0=0, y1=None):
-    """Photo-like RGBA frames (SYN-v1 structure with a counter-based hash in
-    place of the serial xorshift): per-band noise amplitudes 0..256, 1/7 of the
-    16x16 blocks flat, A = 255.  Rows [y0, y1) only, if given."""
-    y1 = H if y1 is None else y1
-    y = torch.arange(y0, y1, device=device, dtype=torch.int64).view(y1 - y0, 1)
-    x = torch.arange(W, device=device, dtype=torch.int64).view(1, W)
-    bx = (200 * x) // max(W - 1, 1)
-    by = (200 * y) // max(H - 1, 1)
-    R = y1 - y0
-    base = [bx.expand(R, W), by.expand(R, W), ((bx + by) // 2)]
-    flat = (((x // 16) + (y // 16)) % 7) == 0
-    amp = torch.tensor(AMP, device=device, dtype=torch.int64)[(8 * y) // H].expand(R, W)
-    idx = y * W + x
-    out = torch.empty((n, R, W, 4), dtype=torch.uint8, device=device)
-    M = 0xFFFFFFFF
-    for f in range(n):
-        for c in range(3):
-            v = (idx * 2654435761 + (seed0 + f) * 40503 + c * 977) & M
-            v = v ^ (v >> 16)
-            v = (v * 0x7FEB352D) & M
-            v = v ^ (v >> 15)
-            v = (v * 0x846CA68B) & M
-            v = v ^ (v >> 16)
-            a = amp.clamp(min=1)
-            noise = torch.where(amp == 0, torch.zeros_like(v),
-                                torch.where(amp < 256, (v % a) - amp // 2, v & 255))
-            val = (base[c] + noise) % 256
-            fv = [40, 80, 120][c]
-            out[f, :, :, c] = torch.where(flat, torch.full_like(val, fv), val).to(torch.uint8)
-        out[f, :, :, 3] = 255
-    return out.view(n, R * W * 4)
+_syn = None
+
+
+def syn_lib():
+    """tools/libnice_syn.so: NICE-SYN-v1 generated on the GPU (xorshift32
+    jump-ahead), bit-identical to the oracle's gen_syn_v1 (tests/test_syn_gen.py)."""
+    global _syn
+    if _syn is None:
+        _syn = ctypes.CDLL(os.path.join(ROOT, "tools", "libnice_syn.so"))
+        _syn.nice_syn_v1_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    return _syn
+
+
+def syn_frames(torch, n, W, H, seed0, device):
+    """n NICE-SYN-v1 RGBA frames, seeds seed0 .. seed0+n-1,
+    generated on `device`: [n, W*H*4] uint8."""
+    out = torch.empty((n, W * H * 4), dtype=torch.uint8, device=device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    rc = syn_lib().nice_syn_v1_dev(ctypes.c_void_p(out.data_ptr()), out.stride(0), n, W, H, 4, seed0, st)
+    if rc != 0:
+        raise RuntimeError(f"nice_syn_v1_dev failed ({rc})")
+    return out
+
+
+def stream_check(O, px, streams, lens, W, H, idx):
+    """Byte-compares the GPU streams of frames `idx` of the measured batch with
+    the oracle's code::encode of the same pixels (outside the timed region)."""
+    L = lens.cpu()
+    for i in idx:
+        want = O.encode(px[i].cpu().numpy(), W, H, 4)
+        got = streams[i, :int(L[i])].cpu().numpy().tobytes()
+        if got != want:
+            raise AssertionError(f"frame {i}: GPU stream differs from the oracle")
+    return f"oracle, {len(idx)} frames of the timed batch (indices {list(idx)}): byte-exact"
 
 
 def cpu_baseline(W, H, seconds=12.0):
     """Oracle (C restatement of the reference, -O3, 1 thread): encode + decode of
-    4K RGBA frames until ~`seconds` of CPU work.  Decode runs on the stream's
+    4K RGBA frames until ~`seconds` of CPU work -- the same frames as the GPU
+    batch's first ones (SYN-v1 seeds 1, 2, ...).  Decode runs on the stream's
     channels=3 view (byte 12 patched), the only form the reference decodes."""
     from oracle import oracle as O
     n = 0
@@ -83,8 +87,8 @@ def cpu_baseline(W, H, seconds=12.0):
         seed += 1
     return {"value": round(n * W * H / t_total / 1e6, 3), "unit": "MPixels/s", "cores": 1,
             "kind": "port",
-            "sample": f"{n} x {W}x{H} RGBA NICE-SYN-v1 frames (seeds 1..{n}), encode+decode, "
-                      f"{t_total:.1f} s single-thread"}
+            "sample": f"{n} x {W}x{H} RGBA NICE-SYN-v1 frames (seeds 1..{n}: frames 0..{n - 1} of the "
+                      f"GPU batch), encode+decode, {t_total:.1f} s single-thread"}
 
 
 def cpu_baseline_threads(W, H, seconds=8.0):
@@ -166,9 +170,7 @@ def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
     W = H = side
     lo, hi = S.band_tiles(W, H, rank, world)
     p0, p1 = S.band_pixels(W, H, lo, hi)
-    y0, y1 = p0 // W, (p1 + W - 1) // W
-    rows = syn_frames(torch, 1, W, H, 11, device, y0, y1).view(-1)
-    px = rows[(p0 - y0 * W) * 4:(p1 - y0 * W) * 4]
+    px = syn_frames(torch, 1, W, H, 11, device).view(-1)[p0 * 4:p1 * 4]
     be = S.HipBands(device.index or 0)
     cdev = "cpu" if dist.get_backend() == "gloo" else None   # where collective tensors live
     out = S.encode_sharded(be, dist, px, p0, W, H, 4, device=cdev)   # warmup
@@ -183,6 +185,42 @@ def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
     return {"workload": f"1 x {W}x{H} RGBA image, bands over {world} ranks, RCCL exchanges + gather-v",
             "ms": round(el * 1e3, 3), "mpix_s": round(W * H / el / 1e6, 2),
             "stream_bytes": int(out.numel()) if out is not None else None}
+
+
+def config4_one_gpu(torch, nice, device, side, reps=3):
+    """BASELINE config 4 on one GPU: the side x side RGBA image (SYN-v1 seed 11)
+    encoded whole (one-frame batch) and through the band C ABI in 8 bands in
+    this process (the 8-rank split, exchanges on the host); both streams must
+    be identical."""
+    S = importlib.import_module(PKG + ".sharded")
+    W = H = side
+    img = syn_frames(torch, 1, W, H, 11, device)
+    bound = (nice.encode_bound(W, H) + 255) // 256 * 256
+    out = torch.empty((1, bound), dtype=torch.uint8, device=device)
+    ln = torch.zeros(1, dtype=torch.int64, device=device)
+    ctx = nice.Context(device.index or 0)
+    nice.encode_batch(img, W, H, 4, out, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nice.encode_batch(img, W, H, 4, out, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    t_whole = (time.perf_counter() - t0) / reps
+    flat = img.view(-1)
+    bes = []
+    band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes)   # warmup (contexts, scratch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes)
+    torch.cuda.synchronize()
+    t_band = (time.perf_counter() - t0) / reps
+    n = int(ln[0])
+    same = band.numel() == n and torch.equal(band, out[0, :n])
+    return {"workload": f"1 x {W}x{H} RGBA SYN-v1 image on 1 GPU", "whole_frame_encode_ms": round(t_whole * 1e3, 2),
+            "whole_frame_mpix_s": round(W * H / t_whole / 1e6, 1),
+            "bands8_one_process_encode_ms": round(t_band * 1e3, 2),
+            "band_stream_equals_whole_frame": bool(same), "stream_bytes": n}
 
 
 def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=16, batch=16, depth=3):
@@ -243,7 +281,10 @@ def main():
     ap.add_argument("--streamed-frames", type=int, default=1024,
                     help="config 5: frames streamed from host memory over all ranks (0: skip)")
     ap.add_argument("--sharded-side", type=int, default=16384,
-                    help="N>1: also time one side x side image encoded across the ranks (0: skip)")
+                    help="config 4: one side x side image encoded across the ranks (N>1), or whole and "
+                         "in 8 bands on one GPU (N=1) (0: skip)")
+    ap.add_argument("--check-frames", type=int, default=4,
+                    help="frames of the timed batch byte-compared with the oracle (rank 0)")
     args = ap.parse_args()
 
     import torch
@@ -290,6 +331,12 @@ def main():
         assert torch.equal(dec.view(F, N, 4)[c:c + 64, :, :3], px.view(F, N, 4)[c:c + 64, :, :3]), \
             "round trip mismatch"
     stream_bytes = int(lens.sum())
+    check = None
+    if rank == 0 and args.check_frames > 0:
+        from oracle import oracle as O
+        k = min(args.check_frames, F)
+        idx = sorted({(F - 1) * j // max(k - 1, 1) for j in range(k)})
+        check = stream_check(O, px, streams, lens, W, H, idx)
 
     L.nice_ctx_set_timing(ctx.ptr, 1)
     barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
@@ -310,21 +357,16 @@ def main():
         return (time.perf_counter() - a) / reps
     t_enc = timed(lambda: nice.encode_batch(px, W, H, 4, streams, lens))
     t_dec = timed(lambda: nice.decode_batch(streams, lens, W, H, 4, dec, status))
-    # single-frame latency (one 4K frame, encode then decode)
+    # single-frame latency (one 4K frame): encode, decode, encode then decode
     one_px, one_s, one_l = px[:1], streams[:1], lens[:1]
     one_d, one_st = dec[:1], status[:1]
+    t_one_enc = timed(lambda: nice.encode_batch(one_px, W, H, 4, one_s, one_l), reps=5)
+    t_one_dec = timed(lambda: nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st), reps=3)
     t_one = timed(lambda: (nice.encode_batch(one_px, W, H, 4, one_s, one_l),
                            nice.decode_batch(one_s, one_l, W, H, 4, one_d, one_st)), reps=2)
     # measured copy peak: device-to-device copy of the frames
     t_copy = timed(lambda: dec.copy_(px), reps=3)
     copy_gb_s = 2 * px.numel() / t_copy / 1e9
-
-    sharded = None
-    if world > 1 and args.sharded_side:
-        try:
-            sharded = sharded_image(torch, nice, dist, device, args.sharded_side, rank, world)
-        except Exception as exc:   # report, never lose the main measurement
-            sharded = {"error": repr(exc)[:300]}
 
     stream_leg = None
     if args.streamed_frames:
@@ -332,6 +374,18 @@ def main():
             stream_leg = streamed(torch, nice, dist, device, px, W, H, rank, world, args.streamed_frames)
         except Exception as exc:   # report, never lose the main measurement
             stream_leg = {"error": repr(exc)[:300]}
+
+    sharded = None
+    if args.sharded_side:
+        del px, streams, dec
+        torch.cuda.empty_cache()
+        try:
+            if world > 1:
+                sharded = sharded_image(torch, nice, dist, device, args.sharded_side, rank, world)
+            else:
+                sharded = config4_one_gpu(torch, nice, device, args.sharded_side)
+        except Exception as exc:   # report, never lose the main measurement
+            sharded = {"error": repr(exc)[:300]}
 
     names = [L.nice_phase_name(i).decode() for i in range(32)]
     phase = {names[i]: {"ms_total": round(ms[i], 3), "launches": int(cnt[i])}
@@ -361,7 +415,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (SYN-v1-structured photo-like RGBA frames generated on device)",
+        "data": "synthetic: NICE-SYN-v1 RGBA frames (SURVEY.md §8d, seeds 1+rank*F ..), generated on device "
+                "bit-identical to the oracle's generator",
         "config": {"workload": f"{F} x {W}x{H} RGBA frames per GPU per step, encode then decode, "
                                f"inputs resident in HBM", "width": W, "height": H,
                    "channels": 4, "frames_per_gpu_per_step": F,
@@ -379,10 +434,13 @@ def main():
         "encode_mpix_s": round(F * N / t_enc / 1e6, 2),
         "decode_mpix_s": round(F * N / t_dec / 1e6, 2),
         "single_frame_latency_ms": round(t_one * 1e3, 2),
+        "single_frame_encode_ms": round(t_one_enc * 1e3, 3),
+        "single_frame_decode_ms": round(t_one_dec * 1e3, 3),
+        "stream_check": check,
         "stream_bytes_per_frame": stream_bytes // F,
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,
-        "sharded_image_encode": sharded,
+        "sharded_image_encode": sharded,   # config 4 (N>1: across ranks; N=1: one GPU)
         "streamed_host_frames": stream_leg,
         "cpu_baseline": None,
         "cpu_baseline_threads": None,

@@ -60,7 +60,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
   L.o_hist = take((size_t)n_frames * N_BINS * 4);
-  L.o_flags = take((size_t)n_frames * 4);
+  L.o_flags = take((size_t)n_frames * 4 + 4);   // + one word: any frame FLAG_LONG
   L.zero_bytes = align_up(o, 16);
   L.o_first = take((size_t)n_frames * T * 4);
   L.o_last = take((size_t)n_frames * T * 4);

@@ -781,7 +781,10 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
       prev = aob;
     }
     a.stream_max[(uint64_t)f * N_STREAMS + s] = (uint8_t)my_max;
-    if (my_emit_max > FAST_MAX_CODE_BITS) atomicOr(&a.frame_flags[f], FLAG_LONG);
+    if (my_emit_max > FAST_MAX_CODE_BITS) {
+      atomicOr(&a.frame_flags[f], FLAG_LONG);
+      atomicOr(&a.frame_flags[a.n_frames], FLAG_LONG);   // any frame of the batch
+    }
   }
 }
 
@@ -1372,6 +1375,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
   __shared__ RecBinTable rbt;
+  if (!(a.frame_flags[a.n_frames] & FLAG_LONG)) return;   // no long-code frame in the batch
   rbt_init(rbt, threadIdx.x);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t N = (int64_t)a.W * a.H;

@@ -212,3 +212,38 @@ def encode_sharded(backend, dist, px, px0: int, width: int, height: int, channel
             q.wait()
     cat = torch.cat(parts) if parts else words.new_zeros(0)
     return backend.assemble(cat.to(words.device), bit0s, bitss, width, height)
+
+
+def encode_bands(px, width: int, height: int, channels: int, n_bands: int, device: int = 0,
+                 backends: list | None = None):
+    """The band C ABI driven in ONE process: ``n_bands`` bands (the split
+    ``n_bands`` ranks would use), each with its own context, the exchange steps
+    done on the host.  ``px``: the whole image (uint8 cuda tensor).  Returns
+    the stream (uint8 cuda tensor), equal to encoding the image whole.
+    ``backends``: reuse contexts across calls (a list, filled on first use)."""
+    import torch
+    from . import _Ctx
+    w, h, c, R = width, height, channels, n_bands
+    N = w * h
+    if backends is None:
+        backends = []
+    while len(backends) < R:
+        be = HipBands(device)
+        be.ctx = _Ctx(device)   # a context holds one band's state between the steps
+        backends.append(be)
+    bands = backends[:R]
+    ranges = [band_tiles(w, h, r, R) for r in range(R)]
+    firsts = []
+    for be, (lo, hi) in zip(bands, ranges):
+        p0, p1 = band_pixels(w, h, lo, hi)
+        firsts.append(int(be.classify(px[p0 * c: p1 * c], p0, w, h, c, c, lo, hi)[0]))
+    hist = None
+    for r, be in enumerate(bands):
+        later = [f for f in firsts[r + 1:] if f != NONE]
+        hr = be.runs(later[0] if later else N)
+        hist = hr.clone() if hist is None else hist + hr
+    bits, seeds = zip(*[be.tables(hist) for be in bands])
+    assert len(set(seeds)) == 1
+    bit0s = [seeds[0] + sum(bits[:r]) for r in range(R)]
+    words = torch.cat([be.pack(bit0s[r], bits[r]) for r, be in enumerate(bands)])
+    return bands[0].assemble(words, bit0s, list(bits), w, h)

@@ -37,27 +37,6 @@ def nice():
 
 
 def band_encode(nice, t, w, h, c, R):
-    """One image through the band C ABI (include/nice.h, config 4) in one
-    process: R bands, each with its own context, the exchange steps done on
-    the host as the ranks' collectives would.  Returns the assembled stream."""
-    import torch
+    """One image through the band C ABI in one process (sharded.encode_bands)."""
     S = importlib.import_module(PKG_NAME + ".sharded")
-    N = w * h
-    bands = [S.HipBands(0) for _ in range(R)]
-    for be in bands:
-        be.ctx = nice._Ctx(0)
-    ranges = [S.band_tiles(w, h, r, R) for r in range(R)]
-    firsts = []
-    for be, (lo, hi) in zip(bands, ranges):
-        p0, p1 = S.band_pixels(w, h, lo, hi)
-        firsts.append(int(be.classify(t[p0 * c: p1 * c], p0, w, h, c, c, lo, hi)[0]))
-    hist = None
-    for r, be in enumerate(bands):
-        later = [f for f in firsts[r + 1:] if f != S.NONE]
-        hr = be.runs(later[0] if later else N)
-        hist = hr.clone() if hist is None else hist + hr
-    bits, seeds = zip(*[be.tables(hist) for be in bands])
-    assert len(set(seeds)) == 1
-    bit0s = [seeds[0] + sum(bits[:r]) for r in range(R)]
-    words = torch.cat([be.pack(bit0s[r], bits[r]) for r, be in enumerate(bands)])
-    return bands[0].assemble(words, bit0s, list(bits), w, h)
+    return S.encode_bands(t, w, h, c, R)
