@@ -183,19 +183,20 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     for (int st = 0; st < N_STREAMS; ++st) { loff[st] = (uint16_t)o; o += 1u << lbits[st]; }
   }
   __syncthreads();
+  // canonical codes (hfe.rs:271-290): one lane per stream, serial in LDS
+  __shared__ uint32_t clo[N_BINS];
+  __shared__ uint8_t clen[N_BINS];
   if (threadIdx.x < N_STREAMS) {
     const int st = threadIdx.x;
     const int n = stream_size(st), b = stream_base(st);
     const uint32_t mx = smax[st];
-    const uint32_t lb = lbits[st];
-    uint16_t* lut = T->lut + loff[st];
     T->max_aob[st] = (uint8_t)mx;
-    T->lut_bits[st] = (uint8_t)lb;
+    T->lut_bits[st] = lbits[st];
     T->lut_off[st] = loff[st];
-    // hfe.rs:271-290 with usize wrapping (shift amounts masked to 6 bits); in
-    // tolerant mode lengths above 31 (zero-count symbols) get no decode entry
-    // (lo above every 31-bit window value) and the decodable codes must fit
-    // their lengths and not overlap
+    // usize wrapping (shift amounts masked to 6 bits); in tolerant mode lengths
+    // above 31 (zero-count symbols) get no decode entry (lo above every 31-bit
+    // window value) and the decodable codes must fit their lengths and not
+    // overlap
     unsigned long long cur = 0;
     uint32_t prev = 0;
     uint64_t prev_lo = ~0ull;
@@ -207,21 +208,12 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
       if (prev > 0) cur += 1;
       const unsigned long long code64 = (1ull << (l & 63u)) - cur - 1ull;
       prev = l;
-      T->sym[b + k] = (uint16_t)sym;
-      T->len[b + k] = (uint8_t)l;
-      if (l > mx) { T->lo[b + k] = 0xFFFFFFFFu; continue; }
-      const uint32_t code = (uint32_t)code64;
-      const uint64_t lo = (uint64_t)code << (mx - l);
+      clen[b + k] = (uint8_t)l;
+      if (l > mx) { clo[b + k] = 0xFFFFFFFFu; continue; }
+      const uint64_t lo = (uint64_t)(uint32_t)code64 << (mx - l);
       if ((code64 >> l) != 0 || (prev_lo != ~0ull && lo + (1ull << (mx - l)) > prev_lo)) ok = false;
       prev_lo = lo;
-      T->lo[b + k] = (uint32_t)lo;
-      // first-level entries
-      if (l <= lb) {
-        const uint32_t e0 = code << (lb - l), e1 = (code + 1) << (lb - l);
-        for (uint32_t e = e0; e < e1 && e < (1u << lb); ++e) lut[e] = (uint16_t)((sym << 5) | l);
-      } else {
-        lut[code >> (l - lb)] = 0;   // long-code marker
-      }
+      clo[b + k] = (uint32_t)lo;
     }
     if (!ok) atomicOr(&bad, 1);
   }
@@ -229,6 +221,31 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
   if (bad) {
     if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_UNSUPPORTED);
     return;
+  }
+  for (int i = threadIdx.x; i < N_BINS; i += 256) {
+    T->lo[i] = clo[i];
+    T->sym[i] = order[i];
+    T->len[i] = clen[i];
+  }
+  // first-level entries, all streams in parallel: entry e of stream st is the
+  // window value x = e << (max - width); the code covering it is the first in
+  // canonical order (lower bounds descending) with lo <= x -- a complete,
+  // non-overlapping code (checked above) covers every x exactly once.  A code
+  // longer than the width leaves the long-code marker 0.
+  const uint32_t n_lut = (uint32_t)loff[N_STREAMS - 1] + (1u << lbits[N_STREAMS - 1]);
+  for (uint32_t e = threadIdx.x; e < n_lut; e += 256) {
+    int st = 0;
+    while (st + 1 < N_STREAMS && e >= loff[st + 1]) ++st;
+    const uint32_t lb = lbits[st], mx = smax[st];
+    const uint32_t x = (e - loff[st]) << (mx - lb);
+    int lo = stream_base(st), hi = lo + stream_size(st) - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (clo[mid] <= x) hi = mid;
+      else lo = mid + 1;
+    }
+    const uint32_t l = clen[lo];
+    T->lut[e] = l <= lb ? (uint16_t)(((uint32_t)order[lo] << 5) | l) : (uint16_t)0;
   }
   if (threadIdx.x == 0) a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
 }

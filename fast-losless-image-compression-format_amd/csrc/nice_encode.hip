@@ -735,8 +735,14 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
   for (int i = lane; i < n; i += 64) counts[i] = a.hist[(uint64_t)f * N_BINS + sb + i];
   for (int i = lane; i < 2 * MAX_ALPHABET + 2; i += 64) h.parent[i] = -1;
   __syncthreads();
+#ifdef NICE_PROF_TABLES
+  const long long pt0 = clock64();
+#endif
   if (lane == 0) huffman_merge_tree(h, counts, n);
   __syncthreads();
+#ifdef NICE_PROF_TABLES
+  const long long pt1 = clock64();
+#endif
   // aob = 1 + number of merged ancestors (u8 wrapping, hfe.rs:79-82)
   uint32_t my_max = 0, my_emit_max = 0;
   for (int i = lane; i < n; i += 64) {
@@ -764,6 +770,9 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
     my_emit_max = max(my_emit_max, (uint32_t)__shfl_xor((int)my_emit_max, o));
   }
   __syncthreads();
+#ifdef NICE_PROF_TABLES
+  const long long pt2 = clock64();
+#endif
   if (lane == 0) {
     // hfe.rs:271-290 with usize wrapping arithmetic
     unsigned long long cur = 0;
@@ -781,6 +790,11 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
       prev = aob;
     }
     a.stream_max[(uint64_t)f * N_STREAMS + s] = (uint8_t)my_max;
+#ifdef NICE_PROF_TABLES
+    const long long pt3 = clock64();
+    if (f == 0) printf("enc_tables stream %d n %d: merge %lld depth+rank %lld canon %lld cycles; wall %lld\n", s, n,
+                       pt1 - pt0, pt2 - pt1, pt3 - pt2, (long long)wall_clock64());
+#endif
     if (my_emit_max > FAST_MAX_CODE_BITS) {
       atomicOr(&a.frame_flags[f], FLAG_LONG);
       atomicOr(&a.frame_flags[a.n_frames], FLAG_LONG);   // any frame of the batch

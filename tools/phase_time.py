@@ -1,0 +1,43 @@
+"""Diagnostic: per-phase HIP-event times of encode + decode for a batch of F
+4K RGBA SYN-v1 frames (F=1: single-frame latency).  Usage: phase_time.py F [reps]"""
+import ctypes, importlib, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import bench
+nice = importlib.import_module("fast-losless-image-compression-format_amd")
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+W, H = 3840, 2160
+dev = torch.device("cuda", 0)
+px = bench.syn_frames(torch, F, W, H, 1, dev)
+stride = (nice.encode_bound(W, H) + 255) // 256 * 256
+st = torch.empty((F, stride), dtype=torch.uint8, device=dev)
+ln = torch.zeros(F, dtype=torch.int64, device=dev)
+dec = torch.empty((F, W * H * 4), dtype=torch.uint8, device=dev)
+status = torch.zeros(F, dtype=torch.int32, device=dev)
+L = nice.lib()
+L.nice_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.nice_ctx_read_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+L.nice_phase_name.restype = ctypes.c_char_p
+ctx = nice._ctx(0)
+for _ in range(2):
+    nice.encode_batch(px, W, H, 4, st, ln)
+    nice.decode_batch(st, ln, W, H, 4, dec, status)
+torch.cuda.synchronize()
+assert int(status.abs().sum()) == 0
+for what, fn in [("encode", lambda: nice.encode_batch(px, W, H, 4, st, ln)),
+                 ("decode", lambda: nice.decode_batch(st, ln, W, H, 4, dec, status))]:
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    L.nice_ctx_set_timing(ctx.ptr, 1)
+    for _ in range(reps):
+        fn()
+    ms = (ctypes.c_double * 32)(); cnt = (ctypes.c_uint32 * 32)()
+    L.nice_ctx_read_timing(ctx.ptr, ms, cnt)
+    L.nice_ctx_set_timing(ctx.ptr, 0)
+    ph = {L.nice_phase_name(i).decode(): round(ms[i] / reps, 4) for i in range(32) if cnt[i]}
+    print(f"{what} F={F}: wall {wall * 1e3:.3f} ms/call ({F * W * H / wall / 1e9:.2f} GPix/s)  phases(ms): {ph}")
