@@ -418,10 +418,11 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
 constexpr int CLS_THREADS = 512;
 constexpr int CLS_PPT = ENC_TILE / CLS_THREADS;   // 2 pixels per thread
 constexpr int CLS_RING = 16384;                   // ring words (64 KB)
-// words 0..7 of the ring mirrored past its end: a neighbour group (pixels
-// b .. b+6 for b = (i - rows*W - 3) mod CLS_RING) is one base address plus
-// immediate offsets, never wrapping
-constexpr int CLS_GUARD = 8;
+// words 0..CLS_GUARD-1 of the ring mirrored past its end: a neighbour group
+// (pixels b .. b+6 for b = ((s - rows*W - 3) mod CLS_RING) + tid, s the
+// wave-uniform part of the pixel index) is one base address plus immediate
+// offsets, never wrapping
+constexpr int CLS_GUARD = CLS_THREADS + 8;
 // luma test offsets in Y space: R,B fields +16, G field +32, plus 256 per field
 constexpr uint32_t LUMA_KY = (256u + 16u) | ((256u + 32u) << 10) | ((256u + 16u) << 20);
 
@@ -447,12 +448,15 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 
 // Branch-free mode decision (every reference valid: i >= 3W+3, W >= 3) from
 // the Y ring; returns the record (same layout as classify_fast).  Four base
-// addresses (rows 0..3 back, 3 pixels left), the rest immediate offsets.
-__device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t i, uint32_t W) {
-  const uint32_t* b0 = ring + ((i - 3u) & (CLS_RING - 1));
-  const uint32_t* b1 = ring + ((i - W - 3u) & (CLS_RING - 1));
-  const uint32_t* b2 = ring + ((i - 2u * W) & (CLS_RING - 1));
-  const uint32_t* b3 = ring + ((i - 3u * W - 3u) & (CLS_RING - 1));
+// addresses (rows 0..3 back, 3 pixels left), the rest immediate offsets: for
+// pixel i = s + tid (s wave-uniform) base k is ring + ((s - c_k) mod RING) +
+// tid, a scalar plus the thread index (the mirrored guard covers the overrun
+// past the ring's end).
+__device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W) {
+  const uint32_t* b0 = ring + ((s - 3u) & (CLS_RING - 1)) + tid;
+  const uint32_t* b1 = ring + ((s - W - 3u) & (CLS_RING - 1)) + tid;
+  const uint32_t* b2 = ring + ((s - 2u * W) & (CLS_RING - 1)) + tid;
+  const uint32_t* b3 = ring + ((s - 3u * W - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t X = b0[3], L = b0[2], L2 = b0[1], L3 = b0[0];
   const uint32_t U = b1[3], UR1 = b1[4], UR3 = b1[6], UL3 = b1[0];
   const uint32_t U2 = b2[0];
@@ -547,12 +551,36 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       v[q] = j < N ? fr[j] : 0u;
     }
   };
+  // this tile's symbol counts (histogram growth since the previous tile), for
+  // enc_tilebits_hist: 858 u16 counts as u32 pairs.  Taken for tile t after
+  // the staging barrier of tile t + 1 (every atomic of t is done, none of t + 1
+  // has started): no barrier of its own.
+  uint64_t prev_t = ~0ull;
+  auto snap_tile = [&]() {
+    if (prev_t != ~0ull && tid < (int)TH_WORDS) {
+      uint32_t wv = 0;
+      if (2 * tid < N_BINS) {
+        const int b = 2 * tid;
+        const uint32_t h0 = hist[b], h1 = hist[b + 1];
+        wv = ((h0 - snap[b]) & 0xFFFFu) | ((h1 - snap[b + 1]) << 16);
+        snap[b] = h0;
+        snap[b + 1] = h1;
+      }
+      a.tile_hist[prev_t * TH_WORDS + tid] = wv;
+    }
+    prev_t = ~0ull;
+  };
   TileIter it(a, w_begin), nx(a, w_begin);
   fetch(nx, pf);
   for (uint64_t w = w_begin; w < w_end; ++w, it.step(1)) {
     const uint32_t f = it.f;
     const uint32_t tt = it.tt();
-    if (f != cur_frame) { flush(cur_frame); cur_frame = f; }
+    if (f != cur_frame) {
+      __syncthreads();
+      snap_tile();
+      flush(cur_frame);
+      cur_frame = f;
+    }
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)min((int64_t)ENC_TILE, N - start);
     // stage this tile (Y space), start loading the next
@@ -565,6 +593,7 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     nx.step(1);
     if (w + 1 < w_end) fetch(nx, pf);
     __syncthreads();
+    snap_tile();
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
     unsigned long long wbal[CLS_PPT];   // coded flags of the wave's 64 pixels per q
@@ -572,7 +601,7 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     for (int q = 0; q < CLS_PPT; ++q) {
       const int p = q * CLS_THREADS + tid;
       const int64_t i = start + p;
-      const uint32_t* bl = ring + ((uint32_t)(i - 1) & (CLS_RING - 1));
+      const uint32_t* bl = ring + ((uint32_t)(start + q * CLS_THREADS - 1) & (CLS_RING - 1)) + tid;
       const bool coded = p < count && (i == 0 || bl[1] != bl[0]);
       const unsigned long long bal = __ballot(coded);
       wbal[q] = bal;
@@ -601,38 +630,46 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     }
     const bool fast = start >= 3 * (int64_t)W + 3;
     uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
+    uint32_t rec[CLS_PPT];
 #pragma unroll
-    for (int q = 0; q < CLS_PPT; ++q) {
+    for (int q = 0; q < CLS_PPT; ++q) {   // both pixels' modes first (independent LDS reads)
       const int p = q * CLS_THREADS + tid;
       const bool coded = (coded_bits >> q) & 1u;
-      uint32_t rec = REC_UNCODED;
+      rec[q] = REC_UNCODED;
       if (fast) {
-        const uint32_t rf = classify_ring(ring, (uint32_t)(start + p), W);
-        rec = coded ? rf : REC_UNCODED;
+        const uint32_t rf = classify_ring(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W);
+        rec[q] = coded ? rf : REC_UNCODED;
       } else if (coded) {
         PixSyms sy;
         RingAcc acc{ring, W, start + p};
         classify<false>((uint32_t)(start + p), W, acc, sy);
-        rec = rec_from_syms(sy);
+        rec[q] = rec_from_syms(sy);
       }
-      if (p < count) recs[p] = rec;
-      {
-        // prefix counts per wave (ballots; lanes 0..4 add them), payload
-        // symbols: four unconditional LDS adds, absent ones into this lane's
-        // discard slot (no divergent branches)
-        uint32_t b0, b1, b2, b3;
-        const uint32_t n = rec_bins(rbt, rec, b0, b1, b2, b3);
-        const uint32_t dump = N_BINS + (uint32_t)lane;
-        {
-          const uint32_t m = rec & 7u;   // REC_UNCODED (7) for run members
-          uint32_t pc = 0;
+    }
 #pragma unroll
-          for (uint32_t k = 0; k < 5; ++k) {
-            const uint32_t c = (uint32_t)__popcll(__ballot(m == k));
-            pc = (uint32_t)lane == k ? c : pc;
-          }
-          if (lane < 5 && pc) atomicAdd(&hist[BIN_PREFIX + lane], pc);
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      if (p < count) recs[p] = rec[q];
+      {
+        // mode prefixes counted per wave (ballots; lanes 0..4 add them).
+        // Measured: per-lane packed counters summed by DPP once per tile were
+        // 8 % slower
+        const uint32_t m = rec[q] & 7u;   // REC_UNCODED (7) for run members
+        uint32_t pc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 5; ++k) {
+          const uint32_t c = (uint32_t)__popcll(__ballot(m == k));
+          pc = (uint32_t)lane == k ? c : pc;
         }
+        if (lane < 5 && pc) atomicAdd(&hist[BIN_PREFIX + lane], pc);
+      }
+      {
+        // payload symbols: four unconditional LDS adds, absent ones into this
+        // lane's discard slot (no divergent branches)
+        uint32_t b0, b1, b2, b3;
+        const uint32_t n = rec_bins(rbt, rec[q], b0, b1, b2, b3);
+        const uint32_t dump = N_BINS + (uint32_t)lane;
         atomicAdd(&hist[coded ? b0 : dump], 1u);
         atomicAdd(&hist[coded && n > 1 ? b1 : dump], 1u);
         atomicAdd(&hist[coded && n > 1 ? b2 : dump], 1u);
@@ -652,21 +689,10 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
         }
       }
     }
-    // this tile's symbol counts (histogram growth since the previous tile),
-    // for enc_tilebits_hist: 858 u16 counts as u32 pairs
-    __syncthreads();
-    if (tid < (int)TH_WORDS) {
-      uint32_t wv = 0;
-      if (2 * tid < N_BINS) {
-        const int b = 2 * tid;
-        const uint32_t h0 = hist[b], h1 = hist[b + 1];
-        wv = ((h0 - snap[b]) & 0xFFFFu) | ((h1 - snap[b + 1]) << 16);
-        snap[b] = h0;
-        snap[b + 1] = h1;
-      }
-      a.tile_hist[((uint64_t)f * T + tt) * TH_WORDS + tid] = wv;
-    }
+    prev_t = (uint64_t)f * T + tt;
   }
+  __syncthreads();
+  snap_tile();
   flush(cur_frame);
 }
 
@@ -1281,28 +1307,17 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
           ++wi;
         }
       };
+      // a pixel's codes composed into one value: 32 bits for every pixel of
+      // the wave (the common case: one put per pixel), else 64 bits (two
+      // puts), else one put per code
+      uint32_t tot[4];
+      uint32_t tmax = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        // the pixel's codes as one value (two puts) when they fit 64 bits
-        uint64_t v = 0;
-        uint32_t tot = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const uint32_t e = Q.e[q][k], n = e & 31u;
-          v = (v << n) | (e >> 5);
-          tot += n;
-        }
-        if (tot <= 64u) {
-          const bool two = tot > 32u;
-          put_n(two ? (uint32_t)(v >> 32) : 0u, two ? tot - 32u : 0u);
-          put_n((uint32_t)v, two ? 32u : tot);
-        } else {
-          put(Q.e[q][0]);
-          put(Q.e[q][1]);
-          put(Q.e[q][2]);
-          put(Q.e[q][3]);
-          put(Q.e[q][4]);
-        }
+        tot[q] = (Q.e[q][0] & 31u) + (Q.e[q][1] & 31u) + (Q.e[q][2] & 31u) + (Q.e[q][3] & 31u) + (Q.e[q][4] & 31u);
+        tmax = max(tmax, tot[q]);
+      }
+      auto put_runs = [&](int q) {
         if (Q.run[q] > 0) {
           uint64_t m = Q.run[q] - 1;
           while (true) {
@@ -1310,6 +1325,41 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
             if (m < 8) break;
             m >>= 3;
           }
+        }
+      };
+      if (__all(tmax <= 32u)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            const uint32_t e = Q.e[q][k];
+            v = (v << (e & 31u)) | (e >> 5);
+          }
+          put_n(v, tot[q]);
+          put_runs(q);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (tot[q] <= 64u) {
+            uint64_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+              const uint32_t e = Q.e[q][k], n = e & 31u;
+              v = (v << n) | (e >> 5);
+            }
+            const bool two = tot[q] > 32u;
+            put_n(two ? (uint32_t)(v >> 32) : 0u, two ? tot[q] - 32u : 0u);
+            put_n((uint32_t)v, two ? 32u : tot[q]);
+          } else {
+            put(Q.e[q][0]);
+            put(Q.e[q][1]);
+            put(Q.e[q][2]);
+            put(Q.e[q][3]);
+            put(Q.e[q][4]);
+          }
+          put_runs(q);
         }
       }
       if (nacc) atomicOr(&bits[wi], (uint32_t)(acc >> 32));

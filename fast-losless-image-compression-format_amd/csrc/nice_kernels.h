@@ -57,7 +57,9 @@ struct EncArgs {
 
 __global__ void enc_classify(EncArgs a);
 __global__ void enc_classify_ring(EncArgs a);
-constexpr uint32_t CLS_RING_MAX_W = 5000;
+// the 16K-pixel ring holds 3W + 3 pixels of references plus two tiles (the one
+// being classified and the next one being staged): 3W + 3 + 2048 <= 16384
+constexpr uint32_t CLS_RING_MAX_W = 4777;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
 constexpr uint32_t DEC_PARSE_THREADS = 512;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring
