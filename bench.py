@@ -223,7 +223,28 @@ def config4_one_gpu(torch, nice, device, side, reps=3):
             "band_stream_equals_whole_frame": bool(same), "stream_bytes": n}
 
 
-def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=16, batch=16, depth=3):
+def gpu_numa_cpus(torch, device):
+    """(NUMA node, its CPUs) of the GPU's PCIe root from sysfs, or (None, None)."""
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as fh:
+            node = int(fh.read().strip())
+        if node < 0:
+            return None, None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as fh:
+            spec = fh.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        return node, cpus & os.sched_getaffinity(0) or None
+    except (OSError, ValueError, AttributeError):
+        return None, None
+
+
+def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=16, batch=32, depth=4,
+             numa_local=True):
     """BASELINE config 5: `total` 4K RGBA frames streamed from host memory over
     the ranks (total / world each): H2D -> encode -> D2H streams, then H2D
     streams -> decode -> D2H pixels, overlapped over `depth` HIP streams
@@ -232,6 +253,12 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     n = total // world
     N = W * H
     k = min(distinct, px.shape[0])
+    # pinned host buffers on the GPU's NUMA node: the host thread runs there
+    # while they are allocated (first touch) and while the copies are issued
+    node, cpus = gpu_numa_cpus(torch, device) if numa_local else (None, None)
+    old_aff = os.sched_getaffinity(0)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
     src = [px[i].cpu().pin_memory() for i in range(k)]
     p = nice.Pipeline(W, H, 4, batch=batch, depth=depth, device=device.index or 0)
     outs = [torch.empty(p.stream_stride, dtype=torch.uint8).pin_memory() for _ in range(k)]
@@ -257,10 +284,13 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     t_enc = max_over_ranks(t_enc, dist, device)
     t_dec = max_over_ranks(t_dec, dist, device)
     p.close()
+    if cpus:
+        os.sched_setaffinity(0, old_aff)
     px_all = n * world * N
     sb = sum(lens[:k]) / k
     return {"workload": f"{n * world} x {W}x{H} RGBA frames from pinned host memory, {n} per GPU, "
                         f"H2D/compute/D2H overlapped ({depth} slots x {batch} frames)",
+            "host_numa_node": node,
             "encode_mpix_s": round(px_all / t_enc / 1e6, 2),
             "decode_mpix_s": round(px_all / t_dec / 1e6, 2),
             "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),

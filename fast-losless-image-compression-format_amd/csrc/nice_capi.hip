@@ -462,7 +462,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
 int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_streams, uint64_t stream_stride,
                             const uint64_t* d_stream_len, const uint64_t* h_stream_len, uint32_t n_frames,
                             uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px, uint64_t px_stride,
-                            uint32_t flags, int32_t* d_status) {
+                            uint32_t flags, int32_t* d_status, uint32_t* h_unsettled) {
   if (!ctx || !d_streams || !d_stream_len || !d_status) return NICE_E_ARG;
   if (out_channels != 3 && out_channels != 4) return NICE_E_ARG;
   if ((stream_stride & 3) || ((uintptr_t)d_streams & 3)) return NICE_E_ARG;
@@ -593,15 +593,25 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   uint32_t host_changed = 1;
   uint32_t it_count = 0;
   const uint32_t max_it = max_chunks + 2;
-  const uint32_t queued = std::min(kSyncQueued, max_it);
+  uint32_t queued = std::min(kSyncQueued, max_it);
+  if (const char* ev = getenv("NICE_DEC_SYNC_QUEUED")) {   // tests: fewer queued iterations
+    const uint32_t v = (uint32_t)atoi(ev);
+    if (v >= 1 && v < queued) queued = v;
+  }
   NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
   for (uint32_t it = 0; it < queued; ++it, ++it_count) {
     tm.begin(NICE_PH_DEC_SYNC, st);
     hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
     tm.end(st);
   }
-  NICE_HIP(hipMemcpyAsync(&host_changed, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
-  NICE_HIP(hipStreamSynchronize(st));
+  if (h_unsettled) {
+    // no host round trip: the caller checks the flag once the stream is done
+    NICE_HIP(hipMemcpyAsync(h_unsettled, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
+    host_changed = 0;
+  } else {
+    NICE_HIP(hipMemcpyAsync(&host_changed, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
+    NICE_HIP(hipStreamSynchronize(st));
+  }
   for (uint32_t it = queued; host_changed && it < max_it; ++it, ++it_count) {
     NICE_HIP(hipMemsetAsync(changed + kSyncFlags - 1, 0, 4, st));
     tm.begin(NICE_PH_DEC_SYNC, st);

@@ -2,6 +2,13 @@
 // BASELINE config 5: frames streamed from host memory, H2D / compute / D2H
 // overlapped on HIP streams).
 //
+// Decode never blocks the host on a chunk: the decoder's sync iterations are
+// queued without a fixpoint check (decode_batch_impl h_unsettled), and a chunk
+// whose parse had not settled -- rare: self-synchronisation normally settles
+// within two or three iterations -- is decoded again, blocking, when its slot
+// is reused.  (The blocking check inside every chunk held back the next
+// chunk's H2D copies behind the previous chunk's first kernels.)
+//
 // The reference codes one image per call from host memory (main.rs:28-75 reads
 // a PNG, code.rs:59-64 encodes it, main.rs:77-103 decodes it back).  Here a
 // caller hands over many host frames at once; they flow through `depth` slots
@@ -45,6 +52,7 @@ struct Slot {
   int32_t* d_status = nullptr;   // batch
   uint64_t* h_len = nullptr;     // pinned, batch
   int32_t* h_status = nullptr;   // pinned, batch
+  uint32_t* h_unsettled = nullptr;   // pinned: decode chunk's parse had not settled
   int64_t chunk = -1;            // chunk in flight (-1: none)
   uint32_t n = 0;                // frames of that chunk
 };
@@ -73,6 +81,7 @@ static void pipe_free(nice_pipe* p) {
     (void)hipFree(s.d_status);
     (void)hipHostFree(s.h_len);
     (void)hipHostFree(s.h_status);
+    (void)hipHostFree(s.h_unsettled);
   }
   delete p;
 }
@@ -109,6 +118,7 @@ extern "C" int nice_pipe_create(int device, uint32_t w, uint32_t h, uint8_t chan
     ok = ok && hipMalloc(&s.d_status, 4ull * batch) == hipSuccess;
     ok = ok && hipHostMalloc(&s.h_len, 8ull * batch, hipHostMallocDefault) == hipSuccess;
     ok = ok && hipHostMalloc(&s.h_status, 4ull * batch, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc(&s.h_unsettled, 4, hipHostMallocDefault) == hipSuccess;
     if (!ok) {
       pipe_free(p);
       return rc != NICE_OK ? rc : NICE_E_HIP;
@@ -194,16 +204,29 @@ extern "C" int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, con
     if (stream_len[f] > p->str_stride) return NICE_E_ARG;
   const uint64_t out_bytes = (uint64_t)p->w * p->h * out_channels;
   const uint32_t nchunks = (n_frames + p->batch - 1) / p->batch;
-  // statuses are read once a slot is reused or at the end
-  auto collect = [&](Slot& s) {
-    if (s.chunk < 0) return;
-    for (uint32_t i = 0; i < s.n; ++i) status[(uint64_t)s.chunk * p->batch + i] = s.h_status[i];
+  // statuses are read once a slot is reused or at the end (its stream done);
+  // an unsettled chunk is decoded again from its device streams, blocking
+  auto collect = [&](Slot& s) -> int {
+    if (s.chunk < 0) return NICE_OK;
+    const uint64_t f0 = (uint64_t)s.chunk * p->batch;
+    if (*s.h_unsettled) {
+      const int rc = nice::decode_batch_impl(s.ctx, s.st, s.d_str, p->str_stride, s.d_len, stream_len + f0, s.n,
+                                             p->w, p->h, out_channels, s.d_px, out_bytes, flags, s.d_status);
+      if (rc != NICE_OK) return rc;
+      for (uint32_t i = 0; i < s.n; ++i)
+        PIPE_HIP(hipMemcpyAsync(px[f0 + i], s.d_px + (uint64_t)i * out_bytes, out_bytes, hipMemcpyDeviceToHost, s.st));
+      PIPE_HIP(hipMemcpyAsync(s.h_status, s.d_status, 4ull * s.n, hipMemcpyDeviceToHost, s.st));
+      PIPE_HIP(hipStreamSynchronize(s.st));
+    }
+    for (uint32_t i = 0; i < s.n; ++i) status[f0 + i] = s.h_status[i];
     s.chunk = -1;
+    return NICE_OK;
   };
   for (uint32_t c = 0; c < nchunks; ++c) {
     Slot& s = p->slots[c % p->depth];
     PIPE_HIP(hipEventSynchronize(s.done));
-    collect(s);
+    int rc = collect(s);
+    if (rc != NICE_OK) return rc;
     const uint32_t n = std::min(p->batch, n_frames - c * p->batch);
     const uint64_t f0 = (uint64_t)c * p->batch;
     for (uint32_t i = 0; i < n; ++i) {
@@ -212,8 +235,9 @@ extern "C" int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, con
                               hipMemcpyHostToDevice, s.st));
     }
     PIPE_HIP(hipMemcpyAsync(s.d_len, s.h_len, 8ull * n, hipMemcpyHostToDevice, s.st));
-    const int rc = nice::decode_batch_impl(s.ctx, s.st, s.d_str, p->str_stride, s.d_len, stream_len + f0, n, p->w,
-                                           p->h, out_channels, s.d_px, out_bytes, flags, s.d_status);
+    *s.h_unsettled = 0;
+    rc = nice::decode_batch_impl(s.ctx, s.st, s.d_str, p->str_stride, s.d_len, stream_len + f0, n, p->w, p->h,
+                                 out_channels, s.d_px, out_bytes, flags, s.d_status, s.h_unsettled);
     if (rc != NICE_OK) return rc;
     for (uint32_t i = 0; i < n; ++i)
       PIPE_HIP(hipMemcpyAsync(px[f0 + i], s.d_px + (uint64_t)i * out_bytes, out_bytes, hipMemcpyDeviceToHost, s.st));
@@ -224,7 +248,8 @@ extern "C" int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, con
   }
   for (Slot& s : p->slots) {
     PIPE_HIP(hipStreamSynchronize(s.st));
-    collect(s);
+    const int rc = collect(s);
+    if (rc != NICE_OK) return rc;
   }
   for (uint32_t f = 0; f < n_frames; ++f)
     if (status[f] != NICE_OK) return status[f];

@@ -58,3 +58,20 @@ def test_pipe_bad_stream_status(nice, O):
     with pytest.raises(nice.NiceError):
         p.decode([good, bad], [good.size, bad.size], outs)
     assert np.array_equal(outs[0], f)
+
+
+def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
+    """One queued sync iteration per chunk: the parse of long slices has not
+    settled when the chunk's kernels are queued, so the pipeline must detect it
+    at slot reuse and decode the chunk again (blocking) -- exact pixels."""
+    monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
+    w, h, c, n = 640, 480, 4, 9
+    frames = _frames(O, n, w, h, c, seed0=40)
+    p = nice.Pipeline(w, h, c, batch=2, depth=2)
+    outs = [np.zeros(p.stream_stride, np.uint8) for _ in range(n)]
+    lens = p.encode(frames, outs)
+    dec = [np.zeros(w * h * c, np.uint8) for _ in range(n)]
+    assert p.decode(outs, lens, dec) == [0] * n
+    for i in range(n):
+        assert np.array_equal(dec[i].reshape(-1, c)[:, :3], frames[i].reshape(-1, c)[:, :3]), i
+    p.close()
