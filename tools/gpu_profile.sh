@@ -16,10 +16,12 @@ cat $O/bench.json
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $S/kt -o run -- \
   python3 $R/bench.py --frames $FR --steps 3 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/kt.log 2>&1
+# counter passes: every dispatch encodes or decodes the same 32 frames (no
+# single-frame or config-4 dispatches in the per-kernel averages)
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "nice::" --output-format csv -d $S/pmc_fetch -o run -- \
-  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_fetch.log 2>&1
+  python3 $R/tools/phase_time.py 32 1 > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "nice::" --output-format csv -d $S/pmc_write -o run -- \
-  python3 $R/bench.py --frames 32 --steps 1 --warmup 1 --no-cpu-baseline --streamed-frames 0 > $O/pmc_write.log 2>&1
+  python3 $R/tools/phase_time.py 32 1 > $O/pmc_write.log 2>&1
 cd $R
 find $S -name "*.csv" -exec ls -la {} \; > $O/files.txt
 cp $(find $S/kt -name "*kernel_stats.csv") $O/kernel_stats.csv
