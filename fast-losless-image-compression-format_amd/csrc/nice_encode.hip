@@ -703,6 +703,8 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
 constexpr int TR_THREADS = 1024;
 __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
   __shared__ uint32_t chunk_min[TR_THREADS];
+  __shared__ uint32_t digits[8];   // run-digit counts, added to the histogram once
+  if (threadIdx.x < 8) digits[threadIdx.x] = 0;
   const uint32_t f = blockIdx.x;
   const uint32_t T = a.tiles_per_frame;
   const uint64_t base = (uint64_t)f * T + a.tile_lo;
@@ -714,6 +716,7 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
   const uint32_t c0 = threadIdx.x * per;
   const uint32_t c1 = min(c0 + per, nt);
   uint32_t m = NONE;
+#pragma unroll 8
   for (uint32_t t = c0; t < c1; ++t) m = min(m, a.tile_first[base + t]);
   chunk_min[threadIdx.x] = m;
   __syncthreads();
@@ -726,6 +729,7 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
     __syncthreads();
   }
   uint32_t nxt = min((threadIdx.x + 1 < TR_THREADS) ? chunk_min[threadIdx.x + 1] : NONE, after);
+#pragma unroll 8
   for (int64_t t = (int64_t)c1 - 1; t >= (int64_t)c0; --t) {
     const uint32_t next_px = (nxt == NONE) ? N : nxt;
     a.tile_next[base + t] = next_px;
@@ -735,7 +739,7 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
       if (run > 0) {
         uint64_t mm = run - 1;
         while (true) {
-          atomicAdd(&a.hist[(uint64_t)f * N_BINS + BIN_PREFIX + P_RUN1 + (uint32_t)(mm & 7u)], 1u);
+          atomicAdd(&digits[mm & 7u], 1u);
           if (mm < 8) break;
           mm >>= 3;
         }
@@ -743,6 +747,9 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
     }
     nxt = min(nxt, a.tile_first[base + t]);
   }
+  __syncthreads();
+  if (threadIdx.x < 8 && digits[threadIdx.x])
+    atomicAdd(&a.hist[(uint64_t)f * N_BINS + BIN_PREFIX + P_RUN1 + threadIdx.x], digits[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1207,6 +1214,7 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   const uint32_t per = (nt + 1023) / 1024;
   const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, nt);
   unsigned long long sum = 0;
+#pragma unroll 8
   for (uint32_t t = c0; t < c1; ++t) sum += a.tile_bits[base + t];
   part[threadIdx.x] = sum;
   __syncthreads();
@@ -1222,6 +1230,7 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   const int64_t seed_word = a.band ? (int64_t)(seed >> 5) - 1 : (int64_t)(seed >> 5);
   uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
   unsigned long long run = seed + (threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+#pragma unroll 8
   for (uint32_t t = c0; t < c1; ++t) {
     a.tile_off[base + t] = run;
     // a word shared with the previous tile (or the header: pre-padded with zeros)

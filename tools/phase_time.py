@@ -1,5 +1,5 @@
 """Diagnostic: per-phase HIP-event times of encode + decode for a batch of F
-4K RGBA SYN-v1 frames (F=1: single-frame latency).  Usage: phase_time.py F [reps]"""
+RGBA SYN-v1 frames (F=1: single-frame latency).  Usage: phase_time.py F [reps [W H]]"""
 import ctypes, importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -7,7 +7,8 @@ import bench
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-W, H = 3840, 2160
+W = int(sys.argv[3]) if len(sys.argv) > 4 else 3840
+H = int(sys.argv[4]) if len(sys.argv) > 4 else 2160
 dev = torch.device("cuda", 0)
 px = bench.syn_frames(torch, F, W, H, 1, dev)
 stride = (nice.encode_bound(W, H) + 255) // 256 * 256
