@@ -429,6 +429,7 @@ def main():
         "dec_reconstruct": out_px_bytes,
     }
     dom = max((k for k in phase if k in algo), key=lambda k: phase[k]["ms_total"])
+    traffic = load_traffic(dom, F)
     avg_s = phase[dom]["ms_total"] / 1e3 / phase[dom]["launches"]
     achieved = algo[dom] / avg_s / 1e9
     total_px = N * F * args.steps * world
@@ -455,7 +456,8 @@ def main():
                      "copy_peak_measured": round(copy_gb_s, 1),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": round(achieved * 1e9 / HBM_PEAK, 5),
-                     "traffic": load_traffic(dom, F),
+                     "traffic": traffic,
+                     "traffic_ratio": round(traffic / algo[dom], 3) if traffic else None,
                      "algo_bytes_per_launch": algo[dom],
                      "avg_launch_ms": round(avg_s * 1e3, 4)},
         # whole path against HBM: encode (px in + stream out) + decode (stream in + px out)
