@@ -52,7 +52,7 @@ struct EncLayout {
   size_t zero_bytes, total;
   size_t o_hist, o_flags;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_thist;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_thist, o_gacc;
 };
 
 EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist = true) {
@@ -79,6 +79,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist
   L.o_toff = take((size_t)n_frames * T * 8);
   L.o_dend = take((size_t)n_frames * 8);
   L.o_thist = take(tile_hist ? (size_t)n_frames * T * TH_WORDS * 4 : 0);
+  L.o_gacc = take((size_t)n_frames * ((T + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES + 1) * 8);
   L.total = o;
   return L;
 }
@@ -245,6 +246,8 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.data_end = (unsigned long long*)(base + L.o_dend);
   a.tile_lo = 0;
   a.tile_hi = T;
+  a.groups = T ? (T + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES : 1;
+  a.gacc = (unsigned long long*)(base + L.o_gacc);
   a.px_lo = 0;
   a.px_hi = (int64_t)N;
   a.band = 0;
@@ -302,7 +305,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
-    hipLaunchKernelGGL(enc_tailruns, dim3(n_frames), dim3(1024), 0, st, a);
+    if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, n_frames), dim3(256), 0, st, a, 0);
+    hipLaunchKernelGGL(enc_tailruns, dim3(a.groups, n_frames), dim3(1024), 0, st, a);
     tm.end(st);
   }
   ctx->timer.begin(NICE_PH_ENC_TABLES, st);
@@ -319,7 +323,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     else hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_TILESCAN, st);
-    hipLaunchKernelGGL(enc_tilescan, dim3(n_frames), dim3(1024), 0, st, a);
+    if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, n_frames), dim3(256), 0, st, a, 1);
+    hipLaunchKernelGGL(enc_tilescan, dim3(a.groups, n_frames), dim3(1024), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_PACK, st);
     hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
@@ -704,6 +709,7 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   a.recs = (uint32_t*)(base + L.o_recs) - band_px0;
   a.tile_lo = tile_lo;
   a.tile_hi = tile_hi;
+  a.groups = (tile_hi - tile_lo + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES;
   a.px_lo = (int64_t)px0;
   a.px_hi = (int64_t)(px0 + px_count);
   a.band = 1;
@@ -728,7 +734,8 @@ int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_
   hipStream_t st = (hipStream_t)stream;
   EncArgs& a = ctx->bs.a;
   a.band_next = band_next;
-  hipLaunchKernelGGL(enc_tailruns, dim3(1), dim3(1024), 0, st, a);
+  if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, 1), dim3(256), 0, st, a, 0);
+  hipLaunchKernelGGL(enc_tailruns, dim3(a.groups, 1), dim3(1024), 0, st, a);
   NICE_HIP(hipMemcpyAsync(d_hist, a.hist, N_BINS * 4, hipMemcpyDeviceToDevice, st));
   NICE_HIP(hipGetLastError());
   return NICE_OK;
@@ -781,7 +788,8 @@ int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_
   a.out = (uint8_t*)d_words - (int64_t)(band_bit0 >> 5) * 4;   // virtual: stream word w at d_words[w - w0]
   a.out_stride = 0;
   const uint32_t tblocks = std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u);
-  hipLaunchKernelGGL(enc_tilescan, dim3(1), dim3(1024), 0, st, a);
+  if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, 1), dim3(256), 0, st, a, 1);
+  hipLaunchKernelGGL(enc_tilescan, dim3(a.groups, 1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);

@@ -700,18 +700,48 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
 // K2: runs crossing tile ends. One block (1024 threads) per frame.
 // tile_next[t] = first coded pixel after tile t (N if none).
 // ---------------------------------------------------------------------------
+// Aggregate of each group of ENC_GROUP_TILES tiles (grid: groups x frames).
+__global__ __launch_bounds__(256) void enc_group_reduce(EncArgs a, int what) {
+  __shared__ unsigned long long part[4];
+  const uint32_t g = blockIdx.x, f = blockIdx.y;
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint32_t t0 = g * ENC_GROUP_TILES, t1 = min(t0 + ENC_GROUP_TILES, nt);
+  const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo;
+  unsigned long long v = what == 0 ? NONE : 0ull;
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += 256) {
+    if (what == 0) v = min(v, (unsigned long long)a.tile_first[base + t]);
+    else v += a.tile_bits[base + t];
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long w = __shfl_xor(v, o);
+    v = what == 0 ? min(v, w) : v + w;
+  }
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long r = part[0];
+    for (int k = 1; k < 4; ++k) r = what == 0 ? min(r, part[k]) : r + part[k];
+    a.gacc[(uint64_t)f * a.groups + g] = r;
+  }
+}
+
 constexpr int TR_THREADS = 1024;
 __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
   __shared__ uint32_t chunk_min[TR_THREADS];
   __shared__ uint32_t digits[8];   // run-digit counts, added to the histogram once
   if (threadIdx.x < 8) digits[threadIdx.x] = 0;
-  const uint32_t f = blockIdx.x;
+  // block (group g, frame f): tiles [g, g + 1) x ENC_GROUP_TILES of the band
+  const uint32_t g = blockIdx.x, f = blockIdx.y;
   const uint32_t T = a.tiles_per_frame;
-  const uint64_t base = (uint64_t)f * T + a.tile_lo;
-  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint32_t ntb = a.tile_hi - a.tile_lo;
+  const uint32_t g0 = g * ENC_GROUP_TILES;
+  const uint64_t base = (uint64_t)f * T + a.tile_lo + g0;
+  const uint32_t nt = min(ntb - g0, ENC_GROUP_TILES);
   const uint32_t N = a.W * a.H;
-  // the first coded pixel after the band (frames: none)
-  const uint32_t after = a.band ? (uint32_t)a.band_next : NONE;
+  // the first coded pixel after the group: later groups, then after the band
+  // (frames: none)
+  uint32_t after = a.band ? (uint32_t)a.band_next : NONE;
+  for (uint32_t k = g + 1; k < a.groups; ++k) after = min(after, (uint32_t)a.gacc[(uint64_t)f * a.groups + k]);
   const uint32_t per = (nt + TR_THREADS - 1) / TR_THREADS;
   const uint32_t c0 = threadIdx.x * per;
   const uint32_t c1 = min(c0 + per, nt);
@@ -1206,11 +1236,16 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
 }
 
 // One 1024-thread block per frame.
+// block (group g, frame f): tiles [g, g + 1) x ENC_GROUP_TILES of the band,
+// from the bits of the earlier groups on
 __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   __shared__ unsigned long long part[1024];
-  const uint32_t f = blockIdx.x;
-  const uint32_t nt = a.tile_hi - a.tile_lo;
-  const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo;
+  const uint32_t g = blockIdx.x, f = blockIdx.y;
+  const uint32_t g0 = g * ENC_GROUP_TILES;
+  const uint32_t nt = min(a.tile_hi - a.tile_lo - g0, ENC_GROUP_TILES);
+  const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo + g0;
+  unsigned long long before = 0;
+  for (uint32_t k = 0; k < g; ++k) before += a.gacc[(uint64_t)f * a.groups + k];
   const uint32_t per = (nt + 1023) / 1024;
   const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, nt);
   unsigned long long sum = 0;
@@ -1229,7 +1264,7 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   const uint64_t seed = a.band ? a.band_bit0 : a.seed_bit[f];
   const int64_t seed_word = a.band ? (int64_t)(seed >> 5) - 1 : (int64_t)(seed >> 5);
   uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
-  unsigned long long run = seed + (threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+  unsigned long long run = seed + before + (threadIdx.x ? part[threadIdx.x - 1] : 0ull);
 #pragma unroll 8
   for (uint32_t t = c0; t < c1; ++t) {
     a.tile_off[base + t] = run;
@@ -1237,8 +1272,8 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
     if ((run & 31) && (int64_t)(run >> 5) > seed_word) out32[run >> 5] = 0u;
     run += a.tile_bits[base + t];
   }
-  if (threadIdx.x == 1023) {
-    const uint64_t end = seed + part[1023];
+  if (threadIdx.x == 1023 && g + 1 == a.groups) {
+    const uint64_t end = seed + before + part[1023];
     a.data_end[f] = end;
     if ((end & 31) && (int64_t)(end >> 5) > seed_word) out32[end >> 5] = 0u;
   }

@@ -53,7 +53,13 @@ struct EncArgs {
   int64_t px_lo, px_hi;
   uint32_t band;
   unsigned long long band_next, band_bit0;
+  // the per-frame tile scans (enc_tailruns, enc_tilescan) run as `groups`
+  // blocks of ENC_GROUP_TILES tiles per frame; gacc holds each group's
+  // aggregate (n_frames * groups: min first coded pixel, then bit total)
+  uint32_t groups;
+  unsigned long long* gacc;
 };
+constexpr uint32_t ENC_GROUP_TILES = 8192;
 
 __global__ void enc_classify(EncArgs a);
 __global__ void enc_classify_ring(EncArgs a);
@@ -70,6 +76,8 @@ __global__ void enc_tilebits(EncArgs a);
 __global__ void enc_tilebits_hist(EncArgs a);
 constexpr uint32_t TH_WORDS = 432;   // u32 words per tile histogram (858 u16 counts, 16-B aligned rows)
 __global__ void enc_tilescan(EncArgs a);
+// group aggregates for the tile scans: what 0 = min of tile_first, 1 = sum of tile_bits
+__global__ void enc_group_reduce(EncArgs a, int what);
 __global__ void enc_pack(EncArgs a);
 __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
