@@ -478,8 +478,15 @@ def main():
         "cpu_baseline_threads": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        try:   # the reference's release profile with target-cpu=native
+            flags = O.use_native()
+        except Exception:
+            flags = "gcc -O3 -march=x86-64-v3 (native build failed)"
         res["cpu_baseline"] = cpu_baseline(W, H, args.cpu_seconds)
         res["cpu_baseline_threads"] = cpu_baseline_threads(W, H, min(args.cpu_seconds, 8.0))
+        res["cpu_baseline"]["build"] = flags
+        res["cpu_baseline_threads"]["build"] = flags
     if rank == 0:
         print(json.dumps(res))
     if dist is not None:

@@ -58,6 +58,17 @@ def build() -> str:
     return _LIB_PATH
 
 
+def use_native() -> str:
+    """Switch to the -march=native build (the timed CPU baseline), compiled on
+    this machine; returns the build's flags, or raises if it cannot be built."""
+    global _lib, _LIB_PATH
+    subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle_native.so"], timeout=120)
+    _LIB_PATH = os.path.join(_HERE, "liboracle_native.so")
+    _lib = None
+    lib()
+    return "gcc -O3 -march=native"
+
+
 def lib():
     global _lib
     if _lib is None:
