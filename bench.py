@@ -397,6 +397,19 @@ def main():
     # measured copy peak: device-to-device copy of the frames
     t_copy = timed(lambda: dec.copy_(px), reps=3)
     copy_gb_s = 2 * px.numel() / t_copy / 1e9
+    # §8 f4: the 5x5 sub-block position map of one frame (8 B written per index)
+    img = nice.Image.new(W, H, 4)
+    pos = img.subblock_positions()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(20):
+        img.subblock_positions(out=pos)
+    ev1.record()
+    torch.cuda.synchronize()
+    t_pos = ev0.elapsed_time(ev1) / 20 / 1e3
+    subblock = {"workload": f"calc_pos_from map of one {W}x{H} frame", "ms": round(t_pos * 1e3, 4),
+                "gb_s": round(8 * N / t_pos / 1e9, 1), "frac": round(8 * N / t_pos / HBM_PEAK, 4)}
+    del pos
 
     stream_leg = None
     if args.streamed_frames:
@@ -469,6 +482,7 @@ def main():
         "single_frame_encode_ms": round(t_one_enc * 1e3, 3),
         "single_frame_decode_ms": round(t_one_dec * 1e3, 3),
         "stream_check": check,
+        "subblock_positions": subblock,
         "stream_bytes_per_frame": stream_bytes // F,
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,

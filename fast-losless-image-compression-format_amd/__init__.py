@@ -105,6 +105,8 @@ def lib():
                                    ctypes.c_void_p, u64, ctypes.c_void_p]
     L.nice_pipe_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u32,
                                    ctypes.c_uint8, ctypes.c_void_p, u32, ctypes.c_void_p]
+    L.nice_subblock_positions_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, u32, u32, u64, u64,
+                                              ctypes.c_void_p]
     _lib = L
     return L
 
@@ -124,6 +126,25 @@ class Image:
     @staticmethod
     def new(width: int, height: int, channels: int) -> "Image":
         return Image(width, height, channels)
+
+    def subblock_positions(self, index0: int = 0, count: int | None = None, device: int = 0, out=None):
+        """image.rs:45-102 calc_pos_from for indices [index0, index0 + count)
+        (default: the whole image), computed on the GPU into an int64 cuda
+        tensor (``out`` or a new one); asynchronous on the current stream."""
+        import torch
+        n = self.width * self.height - index0 if count is None else count
+        if out is None:
+            out = torch.empty(max(n, 0), dtype=torch.int64, device=f"cuda:{device}")
+        if out.numel() < n or out.dtype != torch.int64 or not out.is_contiguous():
+            raise NiceError(E_ARG, "out: contiguous int64 with >= count elements")
+        rc = lib().nice_subblock_positions_dev(device, _stream_ptr(torch, out.device), self.width, self.height,
+                                               index0, n, ctypes.c_void_p(out.data_ptr()))
+        _check(rc, "nice_subblock_positions_dev")
+        return out
+
+    def calc_pos_from(self, index: int) -> int:
+        """image.rs:45-102: raster position of traversal index ``index``."""
+        return int(self.subblock_positions(index, 1)[0])
 
 
 def encode_bound(width: int, height: int) -> int:

@@ -155,6 +155,15 @@ int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, const uint64_t
  * reference CLI (main.rs:28-133) reads and writes PNG with the png crate. */
 int nice_png_unfilter(const uint8_t* raw, uint32_t w, uint32_t h, uint32_t bpp, uint8_t* out);
 
+/* ---- 5x5 sub-block traversal ----
+ * d_pos[i] = Image::new(w, h, _).calc_pos_from(index0 + i) for i < count
+ * (image.rs:45-102), computed on `device`, asynchronous on `stream`.  The
+ * reference's map exactly: not a permutation when w % 5 and h % 5 are both
+ * nonzero, and positions >= w*h for some shapes (w = 7, ...).  w == 0 is
+ * NICE_E_ARG (the reference divides by zero).  The codec does not use it. */
+int nice_subblock_positions_dev(int device, void* stream, uint32_t w, uint32_t h, uint64_t index0,
+                                uint64_t count, uint64_t* d_pos);
+
 /* ---- per-kernel timing (HIP events on the call's stream), for benchmarks ---- */
 enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,

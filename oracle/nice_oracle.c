@@ -1032,3 +1032,33 @@ void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C,
     }
 #undef XS
 }
+
+/* ------------------------------------------------------------------------- */
+/* image.rs:45-102 Image::calc_pos_from (5x5 sub-block boustrophedon order;   */
+/* unused by the reference codec).  usize arithmetic, release wrapping;       */
+/* returns UINT64_MAX where the reference would panic (division by zero).     */
+/* ------------------------------------------------------------------------- */
+uint64_t nice_oracle_calc_pos_from(uint64_t width, uint64_t height, uint64_t index) {
+    const uint64_t SH = 5, SW = 5;                                        /* image.rs:3-4 */
+    const uint64_t h_left = height % SH, w_left = width % SW;             /* image.rs:34-35 */
+    const uint64_t image_size = width * height;                           /* image.rs:36 */
+    const uint64_t width_block_size = width * SH;                         /* image.rs:37 */
+    const uint64_t width_minus_leftover = width - width % SW;             /* image.rs:38 */
+    const uint64_t h_minus_left_times_w = (height - height % SH) * width; /* image.rs:39 */
+    uint64_t sub_h, sub_w, remainder, offset;
+    sub_h = (index >= h_minus_left_times_w && index < image_size) ? h_left : SH;   /* :58-66 */
+    if (width_block_size == 0) return UINT64_MAX;
+    offset = index - index % width_block_size;                            /* :68 */
+    remainder = index - offset;                                           /* :69 */
+    sub_w = (remainder >= sub_h * width_minus_leftover && index < image_size) ? w_left : SW;   /* :71-78 */
+    const uint64_t area = sub_w * sub_h;
+    if (area == 0 || sub_w == 0) return UINT64_MAX;
+    const uint64_t sub_mod2 = (remainder / area) & 1u;                    /* :79 */
+    offset += remainder / area * sub_w;                                   /* :80 */
+    remainder = remainder % area;                                         /* :81 */
+    const uint64_t rows_mod2 = (remainder / sub_w) & 1u;                  /* :83 */
+    if (sub_mod2 == 0) offset += remainder / sub_w * width;               /* :84-88 */
+    else offset += (sub_h - remainder / sub_w - 1) * width;               /* :89-93 */
+    offset += rows_mod2 == 1 ? sub_w - (remainder % sub_w) - 1 : remainder % sub_w;   /* :95 */
+    return offset;
+}

@@ -52,6 +52,7 @@ int nice_oracle_kat_hfe(size_t *stream_len, uint8_t *max_aob);
 
 void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed);
 void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C);
+uint64_t nice_oracle_calc_pos_from(uint64_t width, uint64_t height, uint64_t index);
 void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K);
 
 #ifdef __cplusplus

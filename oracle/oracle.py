@@ -97,6 +97,8 @@ def lib():
                                              ctypes.c_uint32, ctypes.c_uint32]
         L.nice_oracle_gen_gradient.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32,
                                                ctypes.c_uint32]
+        L.nice_oracle_calc_pos_from.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.nice_oracle_calc_pos_from.restype = ctypes.c_uint64
         L.nice_oracle_gen_deep_codes.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         _lib = L
@@ -181,6 +183,11 @@ def gen_deep_codes(width: int, height: int, channels: int, seed: int = 1, k: int
     px = np.zeros(width * height * channels, dtype=np.uint8)
     lib().nice_oracle_gen_deep_codes(_u8p(px), width, height, channels, seed, k)
     return px
+
+
+def calc_pos_from(width: int, height: int, index: int) -> int:
+    """image.rs:45-102 Image::calc_pos_from (2^64-1 where the reference panics)."""
+    return int(lib().nice_oracle_calc_pos_from(width, height, index))
 
 
 def kat_writer() -> bytes:
