@@ -32,7 +32,10 @@ struct DecTables {
   uint8_t len[N_BINS];
   uint8_t max_aob[N_STREAMS];
   uint8_t lut_bits[N_STREAMS];
-  uint8_t pad[18];
+  // 1: no long codes (every first-level entry is a code) and every pixel event
+  // fits 64 bits -- dec_sync decodes an event from one 64-bit window
+  uint8_t fast;
+  uint8_t pad[17];
 };
 static_assert(sizeof(DecTables) % 16 == 0, "per-frame tables stay 16-byte aligned");
 

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/nice.h"
 #include "nice_bits.hpp"
 #include "nice_format.h"
@@ -233,6 +235,9 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
   // non-overlapping code (checked above) covers every x exactly once.  A code
   // longer than the width leaves the long-code marker 0.
   const uint32_t n_lut = (uint32_t)loff[N_STREAMS - 1] + (1u << lbits[N_STREAMS - 1]);
+  __shared__ int lut_hole;
+  if (threadIdx.x == 0) lut_hole = 0;
+  __syncthreads();
   for (uint32_t e = threadIdx.x; e < n_lut; e += 256) {
     int st = 0;
     while (st + 1 < N_STREAMS && e >= loff[st + 1]) ++st;
@@ -246,8 +251,18 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     }
     const uint32_t l = clen[lo];
     T->lut[e] = l <= lb ? (uint16_t)(((uint32_t)order[lo] << 5) | l) : (uint16_t)0;
+    if (l > lb || l == 0) lut_hole = 1;
   }
-  if (threadIdx.x == 0) a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // longest pixel event: the prefix plus the longest payload sequence (code.rs:576-644)
+    const uint32_t m_pay = max(max((uint32_t)smax[S_BACK_REF], 3u * smax[S_RGB]),
+                               max((uint32_t)smax[S_LUMA_REF] + smax[S_LUMA_BASE] + 2u * smax[S_LUMA_OTHER],
+                                   max((uint32_t)smax[S_SMALL_DIFF],
+                                       (uint32_t)smax[S_LUMA2_BASE] + smax[S_LUMA2_R] + smax[S_LUMA2_B])));
+    T->fast = (!lut_hole && smax[S_PREFIX] + m_pay <= 64u) ? 1u : 0u;
+    a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -311,6 +326,7 @@ struct Lane {
   unsigned long long win;
   uint32_t avail;
   uint32_t rp;              // next ring word to shift in
+  uint32_t ws;              // fast parse: stream word held in ring word 0
 };
 // one more pixel event fits in the ring
 __device__ __forceinline__ bool lane_ok(const Lane& L) { return L.rp + PIXEL_WORDS <= RING_W; }
@@ -323,6 +339,7 @@ __device__ __noinline__ void ring_fill_slow(uint32_t* dst, const uint8_t* p, uin
 }
 // Wave-cooperative refill: every lane's ring restarts at the word holding its
 // position (rounded down to 16 bytes).  Must be reached by all 64 lanes.
+template <bool FAST = false>
 __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
                                           Lane& L) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -353,12 +370,30 @@ __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uin
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  const uint32_t* my = wring + lane * RING_STRIDE;
-  const uint32_t o = (uint32_t)(L.pos >> 5) - ws;
-  const uint32_t sh = (uint32_t)(L.pos & 31u);
-  L.win = (((unsigned long long)my[o] << 32) | my[o + 1]) << sh;
-  L.avail = 64u - sh;
-  L.rp = o + 2u;
+  if constexpr (FAST) {
+    L.ws = ws;
+  } else {
+    const uint32_t* my = wring + lane * RING_STRIDE;
+    const uint32_t o = (uint32_t)(L.pos >> 5) - ws;
+    const uint32_t sh = (uint32_t)(L.pos & 31u);
+    L.win = (((unsigned long long)my[o] << 32) | my[o + 1]) << sh;
+    L.avail = 64u - sh;
+    L.rp = o + 2u;
+  }
+}
+
+// Fast parse (DecTables::fast): the event's 64 bits are taken from the ring at
+// its start and every symbol is one table lookup -- no long codes, no top-up.
+__device__ __forceinline__ bool lane_ok_fast(const Lane& L) {
+  return ((uint32_t)(L.pos >> 5) - L.ws) + 3u <= RING_W;
+}
+__device__ __forceinline__ uint32_t fsym(unsigned long long& win, uint32_t& tot, const LutLds& S, uint32_t gp) {
+  const uint32_t v = (uint32_t)(win >> 32);
+  const uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - ((gp >> 16) & 31u)))];
+  const uint32_t n = e & 31u;
+  win <<= n;
+  tot += n;
+  return e >> 5;
 }
 
 // Long code (longer than the LUT width): search of the canonical order.
@@ -434,6 +469,32 @@ __device__ __forceinline__ uint32_t pixel_event(Lane& L, const uint32_t* my, con
       if (lu) s3 = dsym_gp(L, my, S, S_LUMA_OTHER, G.g[S_LUMA_OTHER]);
     }
   }
+  return pfx;
+}
+
+// pixel_event on the fast path: one 64-bit window per event (DecTables::fast
+// bounds every event by 64 bits), no per-symbol refill.
+__device__ __forceinline__ uint32_t pixel_event_fast(Lane& L, const uint32_t* my, const LutLds& S,
+                                                     const StreamParams& G, uint32_t& s0, uint32_t& s1,
+                                                     uint32_t& s2, uint32_t& s3) {
+  const uint32_t o = (uint32_t)(L.pos >> 5) - L.ws;
+  const uint32_t sh = (uint32_t)L.pos & 31u;
+  const uint32_t w0 = my[o], w1 = my[o + 1], w2 = my[o + 2];
+  unsigned long long win = ((((unsigned long long)w0 << 32) | w1) << sh) | (((unsigned long long)w2 << sh) >> 32);
+  uint32_t tot = 0;
+  const uint32_t pfx = fsym(win, tot, S, G.g[PFX_STREAM]);
+  if (pfx < (uint32_t)P_RUN1) {
+    const bool rgb = pfx == (uint32_t)P_RGB, lu = pfx == (uint32_t)P_LUMA, l2 = pfx == (uint32_t)P_LUMA2;
+    const uint32_t gp0 = pfx == (uint32_t)P_BACK_REF ? G.g[S_BACK_REF] : rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_REF]
+                       : l2 ? G.g[S_LUMA2_BASE] : G.g[S_SMALL_DIFF];
+    s0 = fsym(win, tot, S, gp0);
+    if (rgb || lu || l2) {
+      s1 = fsym(win, tot, S, rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_BASE] : G.g[S_LUMA2_R]);
+      s2 = fsym(win, tot, S, rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_OTHER] : G.g[S_LUMA2_B]);
+      if (lu) s3 = fsym(win, tot, S, G.g[S_LUMA_OTHER]);
+    }
+  }
+  L.pos += tot;
   return pfx;
 }
 
@@ -539,45 +600,71 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   Lane L;
   L.pos = D + (e & ((1ull << 40) - 1));
   L.rp = RING_W;   // empty: filled on the first step
+  L.ws = (uint32_t)(L.pos >> 5) - RING_W;   // (fast path) empty as well
   uint32_t dk = (uint32_t)(e >> 44) & 127u;
   uint32_t px = 0, k = 0;
   unsigned long long next_ck = begin + DEC_CK_BITS;
   unsigned long long ck_old = (check && nvalid_old > 0) ? ck[0] : ~0ull;
   bool active = need, synced = false;
-  for (;;) {
-    // at a prefix position: slice end, checkpoint, or one more pixel event
-    if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
-    if (active && L.pos >= next_ck) {
-      const uint32_t cur = (uint32_t)(L.pos - begin) | (dk << 20);
-      if (check && k < nvalid_old && (uint32_t)ck_old == cur) {
-        synced = true;
-        active = false;
-      } else {
-        ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
-        if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
-        ++k;
-        next_ck = k < a.n_ck ? next_ck + DEC_CK_BITS : ~0ull;
-        ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
+  // diagnostics (NICE_DEC_STATS, first pass): wave cycles, refill cycles / count, iterations
+  unsigned long long tw0 = 0, tfill = 0, nfill = 0, nit = 0, nact = 0;
+  const bool tstat = a.stats != nullptr && !check;
+  if (tstat) tw0 = __builtin_amdgcn_s_memtime();
+  // the event loop, instantiated for the fast and the general parse
+  auto parse = [&](auto fast_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
+    for (;;) {
+      // at a prefix position: slice end, checkpoint, or one more pixel event
+      if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
+      if (active && L.pos >= next_ck) {
+        const uint32_t cur = (uint32_t)(L.pos - begin) | (dk << 20);
+        if (check && k < nvalid_old && (uint32_t)ck_old == cur) {
+          synced = true;
+          active = false;
+        } else {
+          ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
+          if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
+          ++k;
+          next_ck = k < a.n_ck ? next_ck + DEC_CK_BITS : ~0ull;
+          ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
+        }
+      }
+      if (!__any(active)) break;
+      if (__any(active && !(FAST ? lane_ok_fast(L) : lane_ok(L)))) {
+        const unsigned long long tf = tstat ? __builtin_amdgcn_s_memtime() : 0;
+        ring_fill<FAST>(wring, p, len, al16, L);
+        if (tstat) { tfill += __builtin_amdgcn_s_memtime() - tf; ++nfill; }
+      }
+      if (tstat) { ++nit; nact += active ? 1u : 0u; }
+      if (active) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        const uint32_t pfx = FAST ? pixel_event_fast(L, my, S, SP, s0, s1, s2, s3)
+                                  : pixel_event(L, my, S, SP, s0, s1, s2, s3);
+        const uint32_t c = pixel_count(pfx, dk);
+        px = sat_add(px, c);
+        if (keep) {
+          const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
+          const uint32_t slot = ne & 3u;
+          if (ne < a.ev_cap && slot == 3u)
+            *reinterpret_cast<uint4*>(evp + ne - 3u) = make_uint4(ev0, ev1, ev2, ev);
+          ev0 = slot == 0u ? ev : ev0;
+          ev1 = slot == 1u ? ev : ev1;
+          ev2 = slot == 2u ? ev : ev2;
+          ++ne;
+        }
       }
     }
-    if (!__any(active)) break;
-    if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
-    if (active) {
-      uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-      const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
-      const uint32_t c = pixel_count(pfx, dk);
-      px = sat_add(px, c);
-      if (keep) {
-        const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
-        const uint32_t slot = ne & 3u;
-        if (ne < a.ev_cap && slot == 3u)
-          *reinterpret_cast<uint4*>(evp + ne - 3u) = make_uint4(ev0, ev1, ev2, ev);
-        ev0 = slot == 0u ? ev : ev0;
-        ev1 = slot == 1u ? ev : ev1;
-        ev2 = slot == 2u ? ev : ev2;
-        ++ne;
-      }
+  };
+  const bool fast = !a.parse_slow && reinterpret_cast<const DecTables*>(a.tables)[f].fast;
+  if (fast) parse(std::true_type{});
+  else parse(std::false_type{});
+  if (tstat) {
+    const unsigned long long tw = __builtin_amdgcn_s_memtime() - tw0;
+    if ((threadIdx.x & 63u) == 0) {
+      atomicAdd(&a.stats[56], tw); atomicAdd(&a.stats[57], tfill); atomicAdd(&a.stats[58], nfill);
+      atomicAdd(&a.stats[59], nit); atomicAdd(&a.stats[61], 1ull);
     }
+    atomicAdd(&a.stats[60], nact);
   }
   if (!need) return;
   if (keep) {

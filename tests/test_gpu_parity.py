@@ -99,6 +99,23 @@ def test_decode_matches(nice, O, case):
         assert np.array_equal(g[:, :3].reshape(-1), ref)
 
 
+@pytest.mark.parametrize("parse", ["fast", "general"])
+def test_decode_parse_paths(nice, O, parse, monkeypatch):
+    """dec_sync decodes a frame whose codes all fit the first-level tables and
+    whose pixel events fit 64 bits from one window per event (DecTables::fast),
+    others symbol by symbol with refills and the long-code search; forcing the
+    general path (NICE_DEC_SLOW_PARSE) must give the same pixels."""
+    if parse == "general":
+        monkeypatch.setenv("NICE_DEC_SLOW_PARSE", "1")
+    for name, px, w, h, c in CASES:
+        if name not in ("syn512x4", "syn1920x1080x4", "grad512x4", "noise300x200x3", "stripes700x300x3",
+                        "palette333x90x3", "wide9000x6x3"):
+            continue
+        got, _ = nice.decode_bytes(O.encode(px, w, h, c))
+        g = np.frombuffer(got, np.uint8).reshape(-1, c)
+        assert np.array_equal(g[:, :3], px.reshape(-1, c)[:, :3]), (name, parse)
+
+
 @pytest.mark.parametrize("case", [c for c in CASES if c[4] == 3], ids=[c[0] for c in CASES if c[4] == 3])
 def test_decode_strict_reference(nice, O, case):
     """STRICT_REFERENCE: fail exactly where the literal reference fails (or may not
