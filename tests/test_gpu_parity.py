@@ -108,8 +108,8 @@ def test_decode_parse_paths(nice, O, parse, monkeypatch):
     if parse == "general":
         monkeypatch.setenv("NICE_DEC_SLOW_PARSE", "1")
     for name, px, w, h, c in CASES:
-        if name not in ("syn512x4", "syn1920x1080x4", "grad512x4", "noise300x200x3", "stripes700x300x3",
-                        "palette333x90x3", "wide9000x6x3"):
+        if name not in ("syn512x4", "syn1920x1080x4", "syn256x3", "odd37x23x4", "noise300x200x3",
+                        "stripes700x300x3", "palette333x90x3", "wide9000x6x3"):
             continue
         got, _ = nice.decode_bytes(O.encode(px, w, h, c))
         g = np.frombuffer(got, np.uint8).reshape(-1, c)
