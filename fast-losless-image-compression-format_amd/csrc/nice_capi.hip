@@ -29,11 +29,13 @@ namespace {
 struct Arena {
   void* ptr = nullptr;
   size_t cap = 0;
+  uint64_t gen = 0;   // bumped by every (re)allocation: contents are unknown after it
   int grow(size_t bytes) {
     if (bytes <= cap) return NICE_OK;
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
+    ++gen;
     if (hipMalloc(&ptr, bytes) != hipSuccess) return NICE_E_HIP;
     cap = bytes;
     return NICE_OK;
@@ -146,6 +148,10 @@ struct nice_ctx {
   Arena enc, dec, host_px, host_out, dev_len, band, band_hdr;
   PhaseTimer timer;
   BandState bs;
+  // decoder record tags (DecArgs::rec_tag): the region the last call used and its tag
+  uint32_t* rec_region = nullptr;
+  uint64_t rec_words = 0, rec_gen = 0;
+  uint32_t rec_epoch = 0;
 };
 
 extern "C" {
@@ -632,7 +638,20 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   tm.end(st);
   tm.begin(NICE_PH_DEC_EMIT, st);
   if (a.ev) hipLaunchKernelGGL(dec_heads, dim3(n_frames), dim3(1024), 0, st, a);
-  NICE_HIP(hipMemsetD32Async((hipDeviceptr_t)a.recs, 1u << 24, (size_t)n_frames * a.rec_stride, st));   // run fill
+  {
+    // run pixels: slots without this call's tag.  Clear (tag 0) only when the
+    // region moved or resized (other data may have held it) or the tags wrap.
+    const uint64_t words = (uint64_t)n_frames * a.rec_stride;
+    if (a.recs != ctx->rec_region || words != ctx->rec_words || ctx->dec.gen != ctx->rec_gen ||
+        ctx->rec_epoch >= 15u || getenv("NICE_DEC_REC_CLEAR")) {
+      NICE_HIP(hipMemsetAsync(a.recs, 0, words * 4, st));
+      ctx->rec_region = a.recs;
+      ctx->rec_words = words;
+      ctx->rec_gen = ctx->dec.gen;
+      ctx->rec_epoch = 0;
+    }
+    a.rec_tag = ++ctx->rec_epoch;
+  }
   hipLaunchKernelGGL(dec_emit, dim3(n_frames * a.emit_blocks), dim3(DEC_PARSE_THREADS), 0, st, a);
   tm.end(st);
   if (a.ev) {

@@ -763,6 +763,14 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
 // (a run pixel is class 1 with c = 0), 4..13 = a pixel in a row above, at
 // (rows back, pixels back) = cls_rows / cls_px.
 constexpr uint32_t REC_RUN = 1u << 24;
+// Records written by a decode call carry its tag (1..15) in bits 28..31; a
+// slot without the current tag (stale, or cleared to 0) is a run pixel.  The
+// record buffer is then cleared only when its tags wrap or its layout changes
+// (nice_capi.hip), not prefilled with REC_RUN by every call.
+constexpr uint32_t REC_TAG_SHIFT = 28;
+__device__ __forceinline__ uint32_t rec_canon(uint32_t r, uint32_t tag) {
+  return (r >> REC_TAG_SHIFT) == tag ? (r & ((1u << REC_TAG_SHIFT) - 1u)) : REC_RUN;
+}
 __host__ __device__ constexpr int cls_rows(int c) {
   return c < 4 ? 0 : c == 4 ? 1 : c == 5 ? 1 : c == 6 ? 2 : c == 7 ? 1 : c <= 10 ? 3 : c == 11 ? 1 : c <= 13 ? 3 : 0;
 }
@@ -977,7 +985,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
       bool bad;
       const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
       if (bad) { err = true; active = false; continue; }
-      G.put(rec, q0, cur, r);
+      G.put(rec, q0, cur, r | (a.rec_tag << REC_TAG_SHIFT));
       q = cur + 1;
       closed = false;
     } else {
@@ -1153,7 +1161,7 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool keep = (uint32_t)k < stop_k || ((uint32_t)k == stop_k && lane < stop_lane);
-      if (keep && i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qk[k]] = r[k];
+      if (keep && i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qk[k]] = r[k] | (a.rec_tag << REC_TAG_SHIFT);
     }
     if (stop_k < 4u) {
       if (lane == 0) err = stop_at_n ? (strict && stop_run) : true;
@@ -1312,7 +1320,7 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
     if (R == 4 && y >= 4 && lane < 3) L.y4tail[lane] = rc.row(y)[W - 3 + lane];
     // this row's records, coalesced
     const uint32_t* rrow = recs + (uint64_t)y * W;
-    for (uint32_t x = lane; x < W; x += 64) recbuf[x] = rrow[x];
+    for (uint32_t x = lane; x < W; x += 64) recbuf[x] = rec_canon(rrow[x], a.rec_tag);
     __syncthreads();
     auto linear_px = [&](int64_t j) -> uint32_t {
       if (j < 0) return 0u;   // pixel 0's left neighbour is itself, not yet written (0)
@@ -1568,7 +1576,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 #pragma unroll
     for (int p = 0; p < S; ++p) {
       const uint32_t x = x0 + p;
-      const uint32_t r = rn[p];
+      const uint32_t r = rec_canon(rn[p], a.rec_tag);
       const uint32_t cls = r >> 24;                          // 0..13
       const uint32_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
       const int dx = (int)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;

@@ -123,6 +123,7 @@ struct DecArgs {
   uint64_t rec_stride;                // W * H rounded up to 4 (16-byte aligned frames)
   uint32_t seg, nseg;
   uint32_t rows_in_lds;               // 1: row ring in LDS, 0: in rowbuf
+  uint32_t rec_tag;                   // 1..15: records of this call carry it in bits 28..31
   uint32_t parse_slow;                // 1: dec_sync ignores DecTables::fast (tests)
   uint32_t* rowbuf;                   // n_frames * R * W (when not in LDS)
   unsigned long long* stats;          // optional diagnostics (NICE_DEC_STATS=1), else null
