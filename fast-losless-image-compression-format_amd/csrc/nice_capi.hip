@@ -693,7 +693,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
             h[50], h[51], h[52], h[53], h[54], h[55], h[56], h[57], a.ev_cap);
     fprintf(stderr, "[nice dec stats] fix-up rounds per row: 0:%llu 1:%llu 2:%llu 3:%llu 4:%llu 5:%llu 6+:%llu\n",
             h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
-    fprintf(stderr, "[nice dec stats] sync first pass: waves=%llu cycles/wave=%.0f refill cycles/wave=%.0f "
+    if (h[61]) fprintf(stderr, "[nice dec stats] sync first pass: waves=%llu cycles/wave=%.0f refill cycles/wave=%.0f "
             "refills/wave=%.1f iterations/wave=%.1f active lane share=%.3f\n",
             h[61], h[61] ? (double)h[56] / h[61] : 0.0, h[61] ? (double)h[57] / h[61] : 0.0,
             h[61] ? (double)h[58] / h[61] : 0.0, h[61] ? (double)h[59] / h[61] : 0.0,
