@@ -328,7 +328,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
-        dist.init_process_group(os.environ.get("NICE_DIST_BACKEND", "nccl"))
+        backend = os.environ.get("NICE_DIST_BACKEND", "nccl")
+        if backend == "nccl":   # RCCL: bind the group to this rank's GPU (eager init, no device guess)
+            dist.init_process_group(backend, device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
     nice = importlib.import_module(PKG)
