@@ -1430,6 +1430,14 @@ constexpr uint32_t ROWS_RING = 4;   // rows y-4 .. y-1 while row y is built
 // current row (index in bits 8..9), unknown until lane 0 has them; none: the
 // constant itself (a reference into a row above, already added).
 constexpr uint32_t W_L1 = 1u << 28, W_AVG = 1u << 31, W_CUR = 1u << 18;   // W_L2, W_L3: bits 29, 30
+// Kind bits >> 28 per record class, 4 bits per class: class 0 is the average
+// (on row 0: the pixel to the left), classes 1-3 the pixel 1-3 back, classes
+// 4-13 a pixel of a row above (no bits; W_CUR is added per pixel).
+constexpr unsigned long long ROWS_KIND = (W_AVG >> 28) | ((unsigned long long)(W_L1 >> 28) << 4) |
+                                         ((unsigned long long)((W_L1 << 1) >> 28) << 8) |
+                                         ((unsigned long long)((W_L1 << 2) >> 28) << 12);
+constexpr unsigned long long ROWS_KIND_Y0 = (ROWS_KIND & ~15ull) | (W_L1 >> 28);
+static_assert((W_AVG >> 28) == 8u && (W_L1 >> 28) == 1u, "kind bits 28..31");
 __device__ __forceinline__ uint32_t wmask(uint32_t w, int bit) {
   return (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1);   // 0 or ~0
 }
@@ -1578,6 +1586,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   for (uint32_t y = 0; y < H; ++y) {
     const unsigned long long c0 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- pre-pass: records -> per-pixel words
+    const unsigned long long kinds = y == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
     uint32_t w[S];
 #pragma unroll
     for (int p = 0; p < S; ++p) {
@@ -1594,10 +1603,11 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const bool cur = up && back == 0;
       // unconditional LDS read (a harmless in-range address for other classes)
       const uint32_t txc = (uint32_t)min(max(tx, 0), (int)W - 1);
-      const uint32_t o = ring[(size_t)((y - back) & (ROWS_RING - 1)) * RS + txc + (txc >> 4)];
+      const uint32_t o = ring[__umul24((y - back) & (ROWS_RING - 1), RS) + txc + (txc >> 4)];
       const uint32_t c = spread3(r & 0xFFFFFFu);
-      const uint32_t kb = cls == 0 ? (y == 0 ? W_L1 : W_AVG)
-                        : cls < 4 ? (W_L1 << (cls - 1u)) : (cur ? W_CUR : 0u);
+      // kind bits from the class (branch-free: the ternary chain compiled to two
+      // nested exec-masked branches per pixel)
+      const uint32_t kb = ((uint32_t)(kinds >> (4u * cls)) & 15u) << 28 | (cur ? W_CUR : 0u);
       w[p] = kb | ((up && !cur) ? ((o + c) & SP_K) : c) | (cur ? ((uint32_t)tx << 8) : 0u);
     }
     // ---- entry: lane 0 exact (previous row's last pixels; 0 before pixel 0)
