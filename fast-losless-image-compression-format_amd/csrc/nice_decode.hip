@@ -1454,9 +1454,12 @@ __device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uin
 }
 
 // Speculative pass over the whole segment; returns the last unknown index.
+// A partial last segment's padding pixels are run records (copies of the pixel
+// before, interval width included), so counting them leaves "every pixel
+// exact" unchanged and spares 16 loop-invariant lane masks (SGPR spills).
 template <int S>
 __device__ __forceinline__ int rows_spec(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
-                                         const uint32_t (&prev)[S], int nvalid) {
+                                         const uint32_t (&prev)[S]) {
   int lu = -1;
 #pragma unroll
   for (int p = 0; p < S; ++p) {
@@ -1464,7 +1467,7 @@ __device__ __forceinline__ int rows_spec(IvS (&v)[S], IvS r0, IvS r1, IvS r2, co
     const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
     const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
     v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
-    lu = (p < nvalid && v[p].len) ? p : lu;
+    lu = v[p].len ? p : lu;
   }
   return lu;
 }
@@ -1474,7 +1477,7 @@ __device__ __forceinline__ int rows_spec(IvS (&v)[S], IvS r0, IvS r1, IvS r2, co
 // has work left.
 template <int S>
 __device__ __forceinline__ int rows_chain(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
-                                          const uint32_t (&prev)[S], int nvalid, int lu, bool go) {
+                                          const uint32_t (&prev)[S], int lu, bool go) {
   int nlu = -1;
   const int upto = go ? lu : -1;
 #pragma unroll
@@ -1487,7 +1490,7 @@ __device__ __forceinline__ int rows_chain(IvS (&v)[S], IvS r0, IvS r1, IvS r2, c
     const bool upd = p <= upto;
     v[p].lo = upd ? n.lo : v[p].lo;
     v[p].len = upd ? n.len : v[p].len;
-    nlu = (upd && p < nvalid && n.len) ? p : nlu;
+    nlu = (upd && n.len) ? p : nlu;
   }
   return go ? nlu : lu;
 }
@@ -1626,7 +1629,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     const unsigned long long c1 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- speculative pass
     IvS v[S];
-    int lu = rows_spec<S>(v, r0, r1, r2, w, prev, nvalid);
+    int lu = rows_spec<S>(v, r0, r1, r2, w, prev);
     if (active) {
       uint32_t* t = tails + lane * 6;
       t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
@@ -1669,7 +1672,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       if (__all(fin || exact_in))   // wave-uniform: every recomputing lane has exact inputs
         lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, !fin);
       else
-        lu = rows_chain<S>(v, r0, r1, r2, w, prev, nvalid, lu, !fin);
+        lu = rows_chain<S>(v, r0, r1, r2, w, prev, lu, !fin);
       if (!fin) {
         if (exact_in && lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         uint32_t* t = tails + lane * 6;
