@@ -517,9 +517,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // single-wave kernel otherwise
   const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
-  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 1)) * 4;
+  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
-  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 1) * 4)
+  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 17) * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
   // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
   // a slice with more parses its events again in dec_emit) unless the scratch

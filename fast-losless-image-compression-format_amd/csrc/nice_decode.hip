@@ -1536,11 +1536,20 @@ __device__ __forceinline__ void rows_barrier() {
   }
 }
 
-__host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 1; }
+// Ring row: W pixels padded one word per 16, plus 16 spare words that take a
+// partial last segment's padding pixels (stored unmasked).
+__host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 17; }
 
 template <int MAXT, bool LDS_RING>
 __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   constexpr int S = ROWS_SEG;
+  // diagnostics counters (NICE_DEC_STATS=1) only in -DNICE_ROWS_STATS builds:
+  // the runtime checks alone held SGPRs and branches in the row loop
+#ifdef NICE_ROWS_STATS
+  unsigned long long* const stats = a.stats;
+#else
+  constexpr unsigned long long* stats = nullptr;
+#endif
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const uint32_t nthr = blockDim.x;
   const uint32_t W = a.W, H = a.H;
@@ -1587,7 +1596,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   __syncthreads();
   unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0, n_fix = 0;
   for (uint32_t y = 0; y < H; ++y) {
-    const unsigned long long c0 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long c0 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- pre-pass: records -> per-pixel words
     const unsigned long long kinds = y == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
     uint32_t w[S];
@@ -1626,7 +1635,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       }
     }
     if (y + 1 < H) load_recs(y + 1);   // in flight during this row
-    const unsigned long long c1 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long c1 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- speculative pass
     IvS v[S];
     int lu = rows_spec<S>(v, r0, r1, r2, w, prev);
@@ -1639,13 +1648,13 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     }
     if (lane == 0) { head3[0] = v[0].lo; head3[1] = v[1].lo; head3[2] = v[2].lo; pend[0] = 0; pend[1] = 0; }
     bool fin = !active || lu < 0;
-    if (a.stats && active && lu >= 0) {
-      atomicAdd(&a.stats[1], 1ull);
-      atomicAdd(&a.stats[3], (unsigned long long)(lu + 1));
-      if (lu >= S - 3) atomicAdd(&a.stats[2], 1ull);
+    if (stats && active && lu >= 0) {
+      atomicAdd(&stats[1], 1ull);
+      atomicAdd(&stats[3], (unsigned long long)(lu + 1));
+      if (lu >= S - 3) atomicAdd(&stats[2], 1ull);
     }
     rows_barrier<LDS_RING>();
-    const unsigned long long c2 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long c2 = stats ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long nfix0 = n_fix;
     // ---- fix-up rounds
     bool cur_done = false;
@@ -1683,19 +1692,18 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         fin = lu < 0 || exact_in;
       }
     }
-    if (a.stats && lane == 0) {
+    if (stats && lane == 0) {
       const unsigned long long r = n_fix - nfix0;
-      atomicAdd(&a.stats[9 + (r >= 6 ? 6 : r)], 1ull);
+      atomicAdd(&stats[9 + (r >= 6 ? 6 : r)], 1ull);
     }
     if (*err) break;
-    const unsigned long long c3 = a.stats ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long c3 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- emit: ring row y (its slot held row y-4, no longer referenced) and the raster
     if (active) {
       uint32_t* rr = ring + (size_t)(y & (ROWS_RING - 1)) * RS + x0 + (x0 >> 4);   // x0 = 16 * lane
       const uint64_t pix = (uint64_t)y * W + x0;
 #pragma unroll
-      for (int p = 0; p < S; ++p)
-        if (p < nvalid) rr[p] = v[p].lo;
+      for (int p = 0; p < S; ++p) rr[p] = v[p].lo;   // padding pixels land in the row's spare words
       if (vec_out && OC == 4) {
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
 #pragma unroll
@@ -1734,16 +1742,16 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 #pragma unroll
     for (int p = 0; p < S; ++p) { prev[p] = v[p].lo; }
     rows_barrier<LDS_RING>();
-    if (a.stats) {
+    if (stats) {
       const unsigned long long c4 = __builtin_amdgcn_s_memtime();
       t_a += c1 - c0; t_b += c2 - c1; t_c += c3 - c2; t_d += c4 - c3;
     }
   }
-  if (a.stats && lane == 0) {
-    atomicAdd(&a.stats[0], (unsigned long long)H);
-    atomicAdd(&a.stats[4], n_fix);
-    atomicAdd(&a.stats[5], t_a); atomicAdd(&a.stats[6], t_b);
-    atomicAdd(&a.stats[7], t_c); atomicAdd(&a.stats[8], t_d);
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], (unsigned long long)H);
+    atomicAdd(&stats[4], n_fix);
+    atomicAdd(&stats[5], t_a); atomicAdd(&stats[6], t_b);
+    atomicAdd(&stats[7], t_c); atomicAdd(&stats[8], t_d);
   }
   if (lane == 0 && *err) set_status(&a.status[f], *err);
 }
