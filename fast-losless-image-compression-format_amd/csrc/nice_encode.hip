@@ -446,39 +446,57 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
   }
 };
 
-// Branch-free mode decision (every reference valid: i >= 3W+3, W >= 3) from
-// the Y ring; returns the record (same layout as classify_fast).  Four base
-// addresses (rows 0..3 back, 3 pixels left), the rest immediate offsets: for
-// pixel i = s + tid (s wave-uniform) base k is ring + ((s - c_k) mod RING) +
-// tid, a scalar plus the thread index (the mirrored guard covers the overrun
-// past the ring's end).
-__device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W) {
+// Branch-free mode decision from the Y ring; returns the record (same layout
+// as classify_fast).  Four base addresses (rows 0..3 back, 3 pixels left), the
+// rest immediate offsets: for pixel i = s + tid (s wave-uniform) base k is
+// ring + ((s - c_k) mod RING) + tid, a scalar plus the thread index (the
+// mirrored guard covers the overrun past the ring's end).
+// HEAD = false: every reference valid (i >= 3W+3, W >= 3).  HEAD = true: the
+// first tiles of a frame, with the reference's validity rules as masks instead
+// of classify<false>'s early exits (code.rs:191-366; W >= 3): a reference
+// counts only if i >= its offset, L is X itself at i = 0, without a row above
+// the prediction is L and LUMA2 is skipped, SMALL_DIFF and LUMA need i > 0, and
+// the raw residual is taken against 0 at i = 0.  (The back reference to pixel
+// i-1 can never hit a coded pixel, so it is not tested.)
+template <bool HEAD>
+__device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
+                                                  uint32_t i) {
   const uint32_t* b0 = ring + ((s - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b1 = ring + ((s - W - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b2 = ring + ((s - 2u * W) & (CLS_RING - 1)) + tid;
   const uint32_t* b3 = ring + ((s - 3u * W - 3u) & (CLS_RING - 1)) + tid;
-  const uint32_t X = b0[3], L = b0[2], L2 = b0[1], L3 = b0[0];
+  const uint32_t X = b0[3], L2 = b0[1], L3 = b0[0];
+  uint32_t L = b0[2];
   const uint32_t U = b1[3], UR1 = b1[4], UR3 = b1[6], UL3 = b1[0];
   const uint32_t U2 = b2[0];
   const uint32_t V = b3[3], VR1 = b3[4], VL1 = b3[2];
   const uint32_t VL3 = b3[0], VR3 = b3[6];
   // back references k = 1..4 (code.rs:191-206; Y equality == RGB equality)
-  const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  const bool has_up = !HEAD || i >= W, has_left = !HEAD || i > 0;
+  if constexpr (HEAD) {
+    e1 = e1 && i >= W;
+    e2 = e2 && i >= W - 1u;
+    e3 = e3 && i >= 2u;
+    e4 = e4 && i >= 2u * W;
+    L = i > 0 ? L : X;
+  }
   const bool br = e1 | e2 | e3 | e4;
   const uint32_t bk = e1 ? 1u : e2 ? 2u : e3 ? 3u : 4u;
-  // prediction floor((U+L)/2) in RGB
+  // prediction floor((U+L)/2) in RGB (L alone without a row above)
   const uint32_t xr = rgb_from_y(X);
-  const uint32_t pred = avg3(rgb_from_y(U), rgb_from_y(L));
+  const uint32_t lrgb = rgb_from_y(L);
+  const uint32_t pred = has_up ? avg3(rgb_from_y(U), lrgb) : lrgb;
   // small diff (code.rs:208-247)
   const uint32_t d = xr + K3(259u) - pred;
-  const bool sd = ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
+  const bool sd = has_left && ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
   const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
   // luma2 against the prediction (code.rs:252-292)
   const uint32_t pg = (pred >> 10) & 0xFFu;
   const uint32_t py = (pred + K3(256u) - (pg | (pg << 20))) & K3(0xFFu);
   const uint32_t xk = X + LUMA_KY;
   const uint32_t t2 = xk - py;
-  const bool l2 = (t2 & LUMA_MASK) == 0;
+  const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins (code.rs:293-339)
   uint32_t lk = 11u, lt = 0u;
   if (__any(!br && !sd && !l2)) {
@@ -486,12 +504,13 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
 #pragma unroll
     for (int k = 10; k >= 0; --k) {
       const uint32_t t = xk - refs[k];
-      const bool ok = (t & LUMA_MASK) == 0;
+      bool ok = (t & LUMA_MASK) == 0;
+      if constexpr (HEAD) ok = ok && i > 0 && i >= (uint32_t)lr_rows(k) * W + (uint32_t)lr_px(k);
       lk = ok ? (uint32_t)k : lk;
       lt = ok ? t : lt;
     }
   }
-  const uint32_t r = xr + K3(256u) - pred;
+  const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
   const uint32_t rec_br = P_BACK_REF | (bk << 3);
   const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
   // LUMA2 and LUMA share the g | r << 6 | b << 11 field layout (LUMA: after its 4-bit reference)
@@ -635,16 +654,12 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     for (int q = 0; q < CLS_PPT; ++q) {   // both pixels' modes first (independent LDS reads)
       const int p = q * CLS_THREADS + tid;
       const bool coded = (coded_bits >> q) & 1u;
-      rec[q] = REC_UNCODED;
-      if (fast) {
-        const uint32_t rf = classify_ring(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W);
-        rec[q] = coded ? rf : REC_UNCODED;
-      } else if (coded) {
-        PixSyms sy;
-        RingAcc acc{ring, W, start + p};
-        classify<false>((uint32_t)(start + p), W, acc, sy);
-        rec[q] = rec_from_syms(sy);
-      }
+      uint32_t rf;
+      if (fast)   // block-uniform: both variants are straight-line code
+        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u);
+      else
+        rf = classify_ring<true>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p));
+      rec[q] = coded ? rf : REC_UNCODED;
     }
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
