@@ -308,6 +308,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
     if (ring) a.tile_hist = (uint32_t*)(base + L.o_thist);
     if (ring) hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    else if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
@@ -744,7 +745,8 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (per < 1) per = 1;
   blocks = (work + per - 1) / per;
   a.tiles_per_block = (uint32_t)per;
-  hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_band_edges, dim3(1), dim3(256), 0, st, a, d_edges);
   NICE_HIP(hipGetLastError());
   ctx->bs = BandState{};

@@ -224,29 +224,40 @@ struct TileIter {
   __device__ __forceinline__ uint64_t tile() const { return (uint64_t)f * T + lo + k; }
 };
 
-// Branch-free mode decision for a pixel whose every reference exists
-// (i >= 3W+3, W >= 3): all tests are evaluated and the first hit in the
-// reference order wins (code.rs:191-366).  Neighbours come from the LDS windows
-// (column col = p + 3 of window `rows`, pixel i - (rows*W + px) at col - px).
-__device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col) {
-  const uint32_t X = tw.w[0][col], L = tw.w[0][col - 1], L2 = tw.w[0][col - 2], L3 = tw.w[0][col - 3];
+// Branch-free mode decision from the LDS windows (column col = p + 3 of window
+// `rows`, pixel i - (rows*W + px) at col - px): all tests are evaluated and the
+// first hit in the reference order wins (code.rs:191-366).  HEAD = false: every
+// reference exists (i >= 3W+3, W >= 3).  HEAD = true (W >= 3): the reference's
+// validity rules as masks, as in classify_ring<true>.
+template <bool HEAD>
+__device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col, uint32_t i, uint32_t W) {
+  const uint32_t X = tw.w[0][col], L2 = tw.w[0][col - 2], L3 = tw.w[0][col - 3];
+  uint32_t L = tw.w[0][col - 1];
   const uint32_t U = tw.w[1][col], UR1 = tw.w[1][col + 1], UR3 = tw.w[1][col + 3], UL3 = tw.w[1][col - 3];
   const uint32_t U2 = tw.w[2][col];
   const uint32_t V = tw.w[3][col], VR1 = tw.w[3][col + 1], VL1 = tw.w[3][col - 1];
   const uint32_t VL3 = tw.w[3][col - 3], VR3 = tw.w[3][col + 3];
   // back references k = 1..4 (k = 0, the pixel before, never equals a coded pixel)
-  const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  const bool has_up = !HEAD || i >= W, has_left = !HEAD || i > 0;
+  if constexpr (HEAD) {
+    e1 = e1 && i >= W;
+    e2 = e2 && i >= W - 1u;
+    e3 = e3 && i >= 2u;
+    e4 = e4 && i >= 2u * W;
+    L = i > 0 ? L : X;
+  }
   const bool br = e1 | e2 | e3 | e4;
   const uint32_t bk = e1 ? 1u : e2 ? 2u : e3 ? 3u : 4u;
-  const uint32_t pred = avg3(U, L);
+  const uint32_t pred = has_up ? avg3(U, L) : L;
   // small diff
   const uint32_t d = X + K3(259u) - pred;
-  const bool sd = ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
+  const bool sd = has_left && ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
   const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
   // luma2 against the average
   const uint32_t xk = X + LUMA_K;
   const uint32_t t2 = luma_t(xk, pred);
-  const bool l2 = (t2 & LUMA_MASK) == 0;
+  const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins; skipped when no lane needs it
   uint32_t lk = 11u, lt = 0u;
   if (__any(!br && !sd && !l2)) {
@@ -254,12 +265,13 @@ __device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col) {
 #pragma unroll
     for (int k = 10; k >= 0; --k) {
       const uint32_t t = luma_t(xk, refs[k]);
-      const bool ok = (t & LUMA_MASK) == 0;
+      bool ok = (t & LUMA_MASK) == 0;
+      if constexpr (HEAD) ok = ok && i > 0 && i >= (uint32_t)lr_rows(k) * W + (uint32_t)lr_px(k);
       lk = ok ? (uint32_t)k : lk;
       lt = ok ? t : lt;
     }
   }
-  const uint32_t r = X + K3(256u) - pred;
+  const uint32_t r = X + K3(256u) - (has_left ? pred : 0u);
   const uint32_t rec_br = P_BACK_REF | (bk << 3);
   const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
   const uint32_t rec_l2 = P_LUMA2 | (((t2 >> 10) & 63u) << 3) | ((t2 & 31u) << 9) | (((t2 >> 20) & 31u) << 14);
@@ -269,7 +281,10 @@ __device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col) {
   return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
 }
 
-__global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
+// TINY (W < 3): references wrap inside the window rows; the general
+// classify<false> decides the first 3W+3 pixels (all of a tiny frame).
+template <bool TINY>
+__device__ __forceinline__ void enc_classify_body(const EncArgs& a) {
   __shared__ TileWin tw;
   __shared__ uint32_t hist[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
@@ -356,13 +371,18 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
       const bool coded = (coded_bits >> r) & 1u;
       uint32_t rec = REC_UNCODED;
       if (fast) {
-        const uint32_t rf = classify_fast(tw, p + 3);
+        const uint32_t rf = classify_fast<false>(tw, p + 3, 0u, a.W);
         rec = coded ? rf : REC_UNCODED;
-      } else if (coded) {
-        PixSyms s;
-        WinAcc acc{&tw, p + 3};
-        classify<false>((uint32_t)(start + p), a.W, acc, s);
-        rec = rec_from_syms(s);
+      } else if constexpr (TINY) {
+        if (coded) {
+          PixSyms s;
+          WinAcc acc{&tw, p + 3};
+          classify<false>((uint32_t)(start + p), a.W, acc, s);
+          rec = rec_from_syms(s);
+        }
+      } else {   // block-uniform branch: both variants are straight-line code
+        const uint32_t rf = classify_fast<true>(tw, p + 3, (uint32_t)(start + p), a.W);
+        rec = coded ? rf : REC_UNCODED;
       }
       if (p < count) recs[p] = rec;
       if (coded) {
@@ -396,6 +416,8 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) {
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS)
     if (hist[b]) atomicAdd(&a.hist[(uint64_t)cur_frame * N_BINS + b], hist[b]);
 }
+__global__ __launch_bounds__(ENC_THREADS) void enc_classify(EncArgs a) { enc_classify_body<false>(a); }
+__global__ __launch_bounds__(ENC_THREADS) void enc_classify_tiny(EncArgs a) { enc_classify_body<true>(a); }
 
 // ---------------------------------------------------------------------------
 // K1r: classify, ring-staged (RGBA frames, 3 <= W <= CLS_RING_MAX_W).

@@ -61,7 +61,8 @@ struct EncArgs {
 };
 constexpr uint32_t ENC_GROUP_TILES = 8192;
 
-__global__ void enc_classify(EncArgs a);
+__global__ void enc_classify(EncArgs a);        // W >= 3
+__global__ void enc_classify_tiny(EncArgs a);   // W < 3
 __global__ void enc_classify_ring(EncArgs a);
 // the 16K-pixel ring holds 3W + 3 pixels of references plus two tiles (the one
 // being classified and the next one being staged): 3W + 3 + 2048 <= 16384
