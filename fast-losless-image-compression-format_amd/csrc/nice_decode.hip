@@ -387,9 +387,16 @@ __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uin
 __device__ __forceinline__ bool lane_ok_fast(const Lane& L) {
   return ((uint32_t)(L.pos >> 5) - L.ws) + 3u <= RING_W;
 }
-__device__ __forceinline__ uint32_t fsym(unsigned long long& win, uint32_t& tot, const LutLds& S, uint32_t gp) {
+// Fast-path stream parameter: (32 - table width) | 2 * table offset << 16, so a
+// lookup's byte address is ((v >> shift) << 17 + param) >> 16 (shifts use the
+// low 5 bits of their operand).
+__device__ __forceinline__ uint32_t fast_param(uint32_t gp) {
+  return (32u - ((gp >> 16) & 31u)) | ((gp & 0xFFFFu) << 17);
+}
+__device__ __forceinline__ uint32_t fsym(unsigned long long& win, uint32_t& tot, const LutLds& S, uint32_t fp) {
   const uint32_t v = (uint32_t)(win >> 32);
-  const uint32_t e = S.lut[(gp & 0xFFFFu) + (v >> (32u - ((gp >> 16) & 31u)))];
+  const uint32_t byte = (((v >> (fp & 31u)) << 17) + fp) >> 16;
+  const uint32_t e = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(S.lut) + byte);
   const uint32_t n = e & 31u;
   win <<= n;
   tot += n;
@@ -619,6 +626,10 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   // the event loop, instantiated for the fast and the general parse
   auto parse = [&](auto fast_tag) {
     constexpr bool FAST = decltype(fast_tag)::value;
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < N_STREAMS; ++i) SP.g[i] = fast_param(SP.g[i]);
+    }
     for (;;) {
       // at a prefix position: slice end, checkpoint, or one more pixel event
       if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
