@@ -1366,28 +1366,19 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
       const uint32_t pos = wbase + x - Q.nb;
       uint64_t acc = 0;
       uint32_t nacc = pos & 31u, wi = pos >> 5;
-      auto put = [&](uint32_t e) {
-        const uint32_t n = e & 31u;   // 0: no symbol (e == 0)
-        acc |= (uint64_t)(e >> 5) << ((64u - nacc - n) & 63u);
-        nacc += n;
-        if (nacc >= 32u) {
-          atomicOr(&bits[wi], (uint32_t)(acc >> 32));
-          acc <<= 32;
-          nacc -= 32u;
-          ++wi;
-        }
-      };
-      // n <= 32 bits of val (0 when n == 0)
+      // n <= 32 bits of val (0 when n == 0).  Branch-free: the top word is OR-ed
+      // into LDS on every put (0 while it is not full) -- a divergent flush
+      // branch per code cost more than the extra LDS OR.
       auto put_n = [&](uint32_t val, uint32_t n) {
         acc |= (uint64_t)val << ((64u - nacc - n) & 63u);
         nacc += n;
-        if (nacc >= 32u) {
-          atomicOr(&bits[wi], (uint32_t)(acc >> 32));
-          acc <<= 32;
-          nacc -= 32u;
-          ++wi;
-        }
+        const bool fl = nacc >= 32u;
+        atomicOr(&bits[wi], fl ? (uint32_t)(acc >> 32) : 0u);
+        acc = fl ? (acc << 32) : acc;
+        nacc -= fl ? 32u : 0u;
+        wi += fl ? 1u : 0u;
       };
+      auto put = [&](uint32_t e) { put_n(e >> 5, e & 31u); };   // e == 0: no symbol
       // a pixel's codes composed into one value: 32 bits for every pixel of
       // the wave (the common case: one put per pixel), else 64 bits (two
       // puts), else one put per code
