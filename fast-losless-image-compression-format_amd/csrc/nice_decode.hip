@@ -1598,9 +1598,12 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         const uint4 t = reinterpret_cast<const uint4*>(rrow)[q];
         rn[4 * q] = t.x; rn[4 * q + 1] = t.y; rn[4 * q + 2] = t.z; rn[4 * q + 3] = t.w;
       }
-    } else {
+    } else if (nvalid > 0) {   // a partial last segment
 #pragma unroll
       for (int p = 0; p < S; ++p) rn[p] = p < nvalid ? rrow[p] : REC_RUN;
+    } else {                   // idle lane: no loads (its wave would run the masked path every row)
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = REC_RUN;
     }
   };
   if (H > 0) load_recs(0);
