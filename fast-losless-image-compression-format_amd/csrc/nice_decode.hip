@@ -976,42 +976,59 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
   Lane L;
   L.pos = D + (e & ((1ull << 40) - 1));
   L.rp = RING_W;
+  L.ws = (uint32_t)(L.pos >> 5) - RING_W;   // (fast parse) empty as well
   uint32_t dk = (uint32_t)(e >> 44) & 127u;
   bool closed = (q == N);          // a run completed exactly at N earlier
   bool err = false;
   RecGroup G{~0ull, REC_RUN, REC_RUN, REC_RUN, REC_RUN, 0u};
-  for (;;) {
-    // at a prefix position
-    const bool at_n = q == N && (dk == 0 || closed);   // every pixel accounted for
-    if (active && (L.pos >= end || L.pos >= hard)) active = false;
-    if (!__any(active)) break;
-    if (__any(active && !lane_ok(L))) ring_fill(wring, p, len, al16, L);
-    if (!active) continue;
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
-    if (at_n) {
-      // the reference still reads one more prefix (code.rs:660): a run digit
-      // there makes it copy past its buffer
-      err = err || (strict && pfx >= (uint32_t)P_RUN1);
-      active = false;
-      continue;
+  // the loop, instantiated for the fast and the general parse (as dec_sync)
+  auto emit = [&](auto fast_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
+    if constexpr (FAST) {
+#pragma unroll
+      for (int k = 0; k < N_STREAMS; ++k) SP.g[k] = fast_param(SP.g[k]);
     }
-    const uint32_t cur = q;
-    const uint32_t c = pixel_count(pfx, dk);
-    if (pfx < (uint32_t)P_RUN1) {
-      bool bad;
-      const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
-      if (bad) { err = true; active = false; continue; }
-      G.put(rec, q0, cur, r | (a.rec_tag << REC_TAG_SHIFT));
-      q = cur + 1;
-      closed = false;
-    } else {
-      const unsigned long long qn = (unsigned long long)q + c;
-      if (qn > N) { err = true; active = false; continue; }
-      q = (uint32_t)qn;
-      closed = closed || q == N;
+    for (;;) {
+      // at a prefix position
+      const bool at_n = q == N && (dk == 0 || closed);   // every pixel accounted for
+      if (active && (L.pos >= end || L.pos >= hard)) active = false;
+      if (!__any(active)) break;
+      bool ok;
+      if constexpr (FAST) ok = lane_ok_fast(L);
+      else ok = lane_ok(L);
+      if (__any(active && !ok)) ring_fill<FAST>(wring, p, len, al16, L);
+      if (!active) continue;
+      uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+      uint32_t pfx;
+      if constexpr (FAST) pfx = pixel_event_fast(L, my, S, SP, s0, s1, s2, s3);
+      else pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
+      if (at_n) {
+        // the reference still reads one more prefix (code.rs:660): a run digit
+        // there makes it copy past its buffer
+        err = err || (strict && pfx >= (uint32_t)P_RUN1);
+        active = false;
+        continue;
+      }
+      const uint32_t cur = q;
+      const uint32_t c = pixel_count(pfx, dk);
+      if (pfx < (uint32_t)P_RUN1) {
+        bool bad;
+        const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
+        if (bad) { err = true; active = false; continue; }
+        G.put(rec, q0, cur, r | (a.rec_tag << REC_TAG_SHIFT));
+        q = cur + 1;
+        closed = false;
+      } else {
+        const unsigned long long qn = (unsigned long long)q + c;
+        if (qn > N) { err = true; active = false; continue; }
+        q = (uint32_t)qn;
+        closed = closed || q == N;
+      }
     }
-  }
+  };
+  const bool fast = !a.parse_slow && reinterpret_cast<const DecTables*>(a.tables)[f].fast;
+  if (fast) emit(std::true_type{});
+  else emit(std::false_type{});
   G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
   if (err) set_status(&a.status[f], NICE_E_FORMAT);
 }
