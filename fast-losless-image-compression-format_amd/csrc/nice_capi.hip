@@ -377,7 +377,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_changed = take(4 * kSyncFlags);
   L.o_rowbuf = take(rowbuf);
   // first-pass pixel events (ev_cap per slice, 0: not kept)
-  L.o_ev = take((size_t)n_frames * max_chunks * ev_cap * 4);
+  L.o_ev = take((size_t)n_frames * ((max_chunks + 63) & ~63u) * ev_cap * 4);
   L.o_evck = take(ev_cap ? (size_t)n_frames * n_ck * max_chunks * 4 : 0);
   L.o_evn = take(ev_cap ? (size_t)n_frames * max_chunks * 4 : 0);
   L.o_agree = take(ev_cap ? (size_t)n_frames * max_chunks * 4 : 0);
@@ -657,7 +657,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   tm.end(st);
   if (a.ev) {
     tm.begin(NICE_PH_DEC_PLACE, st);
-    hipLaunchKernelGGL(dec_place, dim3((max_chunks + 3) / 4, n_frames), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(dec_place, dim3((max_chunks + DEC_PLACE_WAVES - 1) / DEC_PLACE_WAVES, n_frames), dim3(64 * DEC_PLACE_WAVES), 0, st, a);
     tm.end(st);
   }
   if (g.lds > 64 * 1024)

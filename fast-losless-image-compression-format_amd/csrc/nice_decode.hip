@@ -544,6 +544,17 @@ __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
   }
 }
 
+// Event layout: the slices of a frame in groups of 64 (one parse wave); a
+// group's events are interleaved in 16-byte quads, quad c of the group's slice
+// l at words (c * 64 + l) * 4.  The first pass keeps every active lane at the
+// same event index, so each of its 16-byte stores is one contiguous 1 KB per
+// wave (a per-slice layout made every store touch 64 lines: +10 % parse time).
+// Frames are padded to a multiple of 64 slices.
+__device__ __forceinline__ uint64_t ev_group(const DecArgs& a, uint32_t f, uint32_t j) {
+  return ((uint64_t)f * ((a.max_chunks + 63u) & ~63u) + (j & ~63u)) * a.ev_cap + (j & 63u) * 4u;
+}
+__device__ __forceinline__ uint32_t ev_word(uint32_t y) { return (y >> 2) * 256u + (y & 3u); }
+
 // Event word of a coded pixel: its prefix and payload symbols as read
 // (SMALL_DIFF index < 343, bytes < 256; LUMA: reference < 11, so its fourth
 // symbol fits bits 7..11); dec_place turns it into a record.
@@ -601,7 +612,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   unsigned long long* ck = a.ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
   // first pass: keep the pixel events (16-byte stores of 4)
   const bool keep = a.ev != nullptr && !check;
-  uint32_t* evp = a.ev + (base + j) * a.ev_cap;
+  uint32_t* evp = a.ev + ev_group(a, f, j);
   uint32_t* evck = a.ev_ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
   uint32_t ne = 0, ev0 = 0, ev1 = 0, ev2 = 0;
   Lane L;
@@ -663,7 +674,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
           const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
           const uint32_t slot = ne & 3u;
           if (ne < a.ev_cap && slot == 3u)
-            *reinterpret_cast<uint4*>(evp + ne - 3u) = make_uint4(ev0, ev1, ev2, ev);
+            *reinterpret_cast<uint4*>(evp + ev_word(ne - 3u)) = make_uint4(ev0, ev1, ev2, ev);
           ev0 = slot == 0u ? ev : ev0;
           ev1 = slot == 1u ? ev : ev1;
           ev2 = slot == 2u ? ev : ev2;
@@ -687,9 +698,10 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
   if (keep) {
     const uint32_t slot = ne & 3u, q0 = ne & ~3u;
     if (ne <= a.ev_cap) {
-      if (slot > 0u) evp[q0] = ev0;
-      if (slot > 1u) evp[q0 + 1] = ev1;
-      if (slot > 2u) evp[q0 + 2] = ev2;
+      uint32_t* t = evp + ev_word(q0);
+      if (slot > 0u) t[0] = ev0;
+      if (slot > 1u) t[1] = ev1;
+      if (slot > 2u) t[2] = ev2;
     }
     a.ev_n[base + j] = ne <= a.ev_cap ? ne : EV_OVERFLOW;
     a.agree[base + j] = 0;
@@ -1113,15 +1125,15 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
   return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
 }
 
-__global__ __launch_bounds__(256) void dec_place(DecArgs a) {
+__global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
   __shared__ uint32_t sdl[343];   // SMALL_DIFF index -> constant (code.rs:230-247)
-  for (uint32_t i = threadIdx.x; i < 343u; i += 256u) {
+  for (uint32_t i = threadIdx.x; i < 343u; i += blockDim.x) {
     const uint32_t rd = i % 7u, t1 = i / 7u;
     sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t f = blockIdx.y, j = blockIdx.x * 4u + (threadIdx.x >> 6);   // grid (slices / 4, frames)
+  const uint32_t f = blockIdx.y, j = blockIdx.x * DEC_PLACE_WAVES + (threadIdx.x >> 6);   // grid (slices / waves, frames)
   if (a.status[f] != 0) return;
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
@@ -1140,7 +1152,7 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
   unsigned long long q = a.chunk_start[base + j] + (ag == 0u ? 0ull : (a.ck[cki] >> 32));
   const uint64_t N = (uint64_t)a.W * a.H;
   if (q > N) return;                    // tail bytes
-  const uint32_t* evp = a.ev + (base + j) * a.ev_cap;
+  const uint32_t* evp = a.ev + ev_group(a, f, j);
   uint32_t* rec = a.recs + (uint64_t)f * a.rec_stride;
   const bool strict = (a.flags & NICE_DEC_STRICT_REFERENCE) != 0;
   bool err = false;
@@ -1148,14 +1160,14 @@ __global__ __launch_bounds__(256) void dec_place(DecArgs a) {
   // record stores), prefix sums per row plus the rows before
   uint32_t nx[4];   // the next step's events, loaded one step ahead
 #pragma unroll
-  for (int k = 0; k < 4; ++k) nx[k] = i_first + 64u * k + lane < nev ? evp[i_first + 64u * k + lane] : 0u;
+  for (int k = 0; k < 4; ++k) nx[k] = i_first + 64u * k + lane < nev ? evp[ev_word(i_first + 64u * k + lane)] : 0u;
   for (uint32_t i = i_first; i < nev; i += 256u) {
     uint32_t ev[4], r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       ev[k] = nx[k];
       const uint32_t y = i + 256u + 64u * k + lane;
-      nx[k] = y < nev ? evp[y] : 0u;
+      nx[k] = y < nev ? evp[ev_word(y)] : 0u;
     }
     unsigned long long c[4], qk[4], carry = 0;
     uint32_t stop_k = 4u, stop_lane = 64u;
