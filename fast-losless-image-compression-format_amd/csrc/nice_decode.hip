@@ -910,7 +910,7 @@ struct RecGroup {
 };
 
 // Lanes take sub-slices of DEC_EMIT_BITS: sub-slice s of slice j starts at the
-// converged parse's checkpoint (s * DEC_EMIT_BITS / 128 - 1) -- a prefix
+// converged parse's checkpoint (s * DEC_EMIT_BITS / DEC_CK_BITS - 1) -- a prefix
 // position with its run digits and pixel count -- so emission parallelism does
 // not depend on the slice size the sync pass uses.  With the first pass's
 // events kept (a.ev), the lanes take dec_heads' list instead and each stops at
