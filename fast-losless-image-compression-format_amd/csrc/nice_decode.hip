@@ -672,12 +672,12 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
         px = sat_add(px, c);
         if (keep) {
           const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
-          const uint32_t slot = ne & 3u;
-          if (ne < a.ev_cap && slot == 3u)
+          // the last three events in a shift register (ev2 the newest)
+          if (ne < a.ev_cap && (ne & 3u) == 3u)
             *reinterpret_cast<uint4*>(evp + ev_word(ne - 3u)) = make_uint4(ev0, ev1, ev2, ev);
-          ev0 = slot == 0u ? ev : ev0;
-          ev1 = slot == 1u ? ev : ev1;
-          ev2 = slot == 2u ? ev : ev2;
+          ev0 = ev1;
+          ev1 = ev2;
+          ev2 = ev;
           ++ne;
         }
       }
@@ -699,9 +699,10 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
     const uint32_t slot = ne & 3u, q0 = ne & ~3u;
     if (ne <= a.ev_cap) {
       uint32_t* t = evp + ev_word(q0);
-      if (slot > 0u) t[0] = ev0;
-      if (slot > 1u) t[1] = ev1;
-      if (slot > 2u) t[2] = ev2;
+      // the last `slot` events are the newest of ev0..ev2
+      if (slot == 3u) { t[0] = ev0; t[1] = ev1; t[2] = ev2; }
+      if (slot == 2u) { t[0] = ev1; t[1] = ev2; }
+      if (slot == 1u) t[0] = ev2;
     }
     a.ev_n[base + j] = ne <= a.ev_cap ? ne : EV_OVERFLOW;
     a.agree[base + j] = 0;
