@@ -181,32 +181,37 @@ __device__ __forceinline__ uint32_t rec_bins(uint32_t rec, uint32_t& b0, uint32_
   b3 = rb_bin(rec, m, 3);
   return (RB_N >> (3u * m)) & 7u;
 }
-// The same from an LDS table (one 16-byte read per record): row m (record
-// bits 0..2; rows 5..7 empty), word k = base | shift << 10 | width << 15, the
-// payload count in bits 20..22 of word 0.
-struct RecBinTable { uint4 row[8]; };
+// The same from an LDS table (two 16-byte reads per record, row m = record
+// bits 0..2; rows 5..7 empty).  v_bfe_u32 reads only the low 5 bits of its
+// offset and width operands, so word a[m].k = shift | base << 16 and word
+// b[m].k = width (the payload count in bits 8..10 of b[m].x): a bin is one
+// shift, one field extract and one add (packing shift and width in one word
+// took two more shifts and a mask per bin).
+struct RecBinTable { uint4 a[8], b[8]; };
 __device__ __forceinline__ void rbt_init(RecBinTable& t, int tid) {
   if (tid < 8) {
-    uint32_t w[4];
+    uint32_t wa[4], wb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t m = (uint32_t)tid;
       const uint32_t base = m < 5 ? (uint32_t)(RB_BASE[k] >> (10u * m)) & 0x3FFu : 0u;
       const uint32_t fw = m < 5 ? (uint32_t)(RB_FIELD[k] >> (10u * m)) & 0x3FFu : 0u;
-      w[k] = base | (fw & 31u) << 10 | (fw >> 5) << 15;
+      wa[k] = (fw & 31u) | base << 16;
+      wb[k] = fw >> 5;
     }
-    w[0] |= (tid < 5 ? (RB_N >> (3u * tid)) & 7u : 0u) << 20;
-    t.row[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+    wb[0] |= (tid < 5 ? (RB_N >> (3u * tid)) & 7u : 0u) << 8;
+    t.a[tid] = make_uint4(wa[0], wa[1], wa[2], wa[3]);
+    t.b[tid] = make_uint4(wb[0], wb[1], wb[2], wb[3]);
   }
 }
 __device__ __forceinline__ uint32_t rec_bins(const RecBinTable& t, uint32_t rec, uint32_t& b0, uint32_t& b1,
                                              uint32_t& b2, uint32_t& b3) {
-  const uint4 r = t.row[rec & 7u];
-  b0 = (r.x & 0x3FFu) + __builtin_amdgcn_ubfe(rec, (r.x >> 10) & 31u, (r.x >> 15) & 31u);
-  b1 = (r.y & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.y >> 10, r.y >> 15);
-  b2 = (r.z & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.z >> 10, r.z >> 15);
-  b3 = (r.w & 0x3FFu) + __builtin_amdgcn_ubfe(rec, r.w >> 10, r.w >> 15);
-  return r.x >> 20;
+  const uint4 ra = t.a[rec & 7u], rb = t.b[rec & 7u];
+  b0 = (ra.x >> 16) + __builtin_amdgcn_ubfe(rec, ra.x, rb.x);
+  b1 = (ra.y >> 16) + __builtin_amdgcn_ubfe(rec, ra.y, rb.y);
+  b2 = (ra.z >> 16) + __builtin_amdgcn_ubfe(rec, ra.z, rb.z);
+  b3 = (ra.w >> 16) + __builtin_amdgcn_ubfe(rec, ra.w, rb.w);
+  return rb.x >> 8;
 }
 
 // Work item -> (frame, tile) without a 64-bit division per tile (one at the
