@@ -285,6 +285,21 @@ constexpr uint32_t RING_STRIDE = 20;   // 80 bytes: 16-byte aligned rings
 constexpr uint32_t RING_QUADS = RING_W / 4;
 constexpr uint32_t PIXEL_WORDS = 5;    // one pixel event: <= 5 symbols of <= 31 bits
 
+constexpr uint32_t PFX_STREAM = S_PREFIX;
+// payload stream i of mode m (code.rs:576-644), 4 bits each at 4 * (4m + i)
+constexpr unsigned long long PAY_STREAMS =
+    ((unsigned long long)S_BACK_REF << 0) |
+    ((unsigned long long)S_RGB << 16) | ((unsigned long long)S_RGB << 20) | ((unsigned long long)S_RGB << 24) |
+    ((unsigned long long)S_LUMA_REF << 32) | ((unsigned long long)S_LUMA_BASE << 36) |
+    ((unsigned long long)S_LUMA_OTHER << 40) | ((unsigned long long)S_LUMA_OTHER << 44) |
+    ((unsigned long long)S_SMALL_DIFF << 48);   // mode 4 (LUMA2): pay_stream
+static_assert(P_BACK_REF == 0 && P_RGB == 1 && P_LUMA == 2 && P_SMALL_DIFF == 3 && P_LUMA2 == 4 &&
+                  P_RUN1 == 5, "prefix numbering");
+__device__ __forceinline__ uint32_t pay_stream(uint32_t m, uint32_t i) {
+  // mode 4 (LUMA2) does not fit the 64-bit table: handled here
+  return m == (uint32_t)P_LUMA2 ? (uint32_t)S_LUMA2_BASE + i : (uint32_t)(PAY_STREAMS >> (4u * (4u * m + i))) & 15u;
+}
+
 struct LutLds {
   uint16_t lut[DEC_LUT_BUDGET];
   uint32_t lo[N_BINS];   // canonical order (long codes): aligned lower bounds,
@@ -292,6 +307,7 @@ struct LutLds {
   uint8_t len[N_BINS];
   uint32_t gp[16];    // per stream: lut_off | lut_bits << 16 | max_aob << 24
   uint32_t gs[16];    // per stream: canonical-order base | alphabet size << 16
+  uint4 pp[8];        // fast parse: per prefix 0..4, the fast_param of its payload streams 0..3
 };
 
 __device__ inline void load_lut(LutLds& S, const DecTables* T) {
@@ -307,6 +323,16 @@ __device__ inline void load_lut(LutLds& S, const DecTables* T) {
     const int st = (int)threadIdx.x;
     S.gp[st] = (uint32_t)T->lut_off[st] | ((uint32_t)T->lut_bits[st] << 16) | ((uint32_t)T->max_aob[st] << 24);
     S.gs[st] = (uint32_t)stream_base(st) | ((uint32_t)stream_size(st) << 16);
+  }
+  if (threadIdx.x < 8u) {   // payload streams of each mode (code.rs:576-644), as fast parameters
+    const uint32_t m = threadIdx.x;
+    uint32_t w[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t st = m < 5u ? pay_stream(m, i) : 0u;
+      w[i] = (32u - T->lut_bits[st]) | ((uint32_t)T->lut_off[st] << 17);
+    }
+    S.pp[m] = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -434,21 +460,6 @@ __device__ __forceinline__ uint32_t dsym_gp(Lane& L, const uint32_t* my, const L
   L.avail += need ? 32u : 0u;
   return e >> 5;
 }
-constexpr uint32_t PFX_STREAM = S_PREFIX;
-// payload stream i of mode m (code.rs:576-644), 4 bits each at 4 * (4m + i)
-constexpr unsigned long long PAY_STREAMS =
-    ((unsigned long long)S_BACK_REF << 0) |
-    ((unsigned long long)S_RGB << 16) | ((unsigned long long)S_RGB << 20) | ((unsigned long long)S_RGB << 24) |
-    ((unsigned long long)S_LUMA_REF << 32) | ((unsigned long long)S_LUMA_BASE << 36) |
-    ((unsigned long long)S_LUMA_OTHER << 40) | ((unsigned long long)S_LUMA_OTHER << 44) |
-    ((unsigned long long)S_SMALL_DIFF << 48);   // mode 4 (LUMA2): pay_stream
-static_assert(P_BACK_REF == 0 && P_RGB == 1 && P_LUMA == 2 && P_SMALL_DIFF == 3 && P_LUMA2 == 4 &&
-                  P_RUN1 == 5, "prefix numbering");
-__device__ __forceinline__ uint32_t pay_stream(uint32_t m, uint32_t i) {
-  // mode 4 (LUMA2) does not fit the 64-bit table: handled here
-  return m == (uint32_t)P_LUMA2 ? (uint32_t)S_LUMA2_BASE + i : (uint32_t)(PAY_STREAMS >> (4u * (4u * m + i))) & 15u;
-}
-
 // One pixel event at a prefix position: the prefix and, for a coded pixel, its
 // payload symbols.  Returns the prefix; s0..s3 receive the payload.
 // The frame's stream parameters (S.gp) held in scalar registers: a payload
@@ -492,13 +503,14 @@ __device__ __forceinline__ uint32_t pixel_event_fast(Lane& L, const uint32_t* my
   const uint32_t pfx = fsym(win, tot, S, G.g[PFX_STREAM]);
   if (pfx < (uint32_t)P_RUN1) {
     const bool rgb = pfx == (uint32_t)P_RGB, lu = pfx == (uint32_t)P_LUMA, l2 = pfx == (uint32_t)P_LUMA2;
-    const uint32_t gp0 = pfx == (uint32_t)P_BACK_REF ? G.g[S_BACK_REF] : rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_REF]
-                       : l2 ? G.g[S_LUMA2_BASE] : G.g[S_SMALL_DIFF];
-    s0 = fsym(win, tot, S, gp0);
+    // the mode's payload parameters in one LDS read (selecting them from
+    // scalar registers by prefix took a move and a select per candidate)
+    const uint4 pp = S.pp[pfx];
+    s0 = fsym(win, tot, S, pp.x);
     if (rgb || lu || l2) {
-      s1 = fsym(win, tot, S, rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_BASE] : G.g[S_LUMA2_R]);
-      s2 = fsym(win, tot, S, rgb ? G.g[S_RGB] : lu ? G.g[S_LUMA_OTHER] : G.g[S_LUMA2_B]);
-      if (lu) s3 = fsym(win, tot, S, G.g[S_LUMA_OTHER]);
+      s1 = fsym(win, tot, S, pp.y);
+      s2 = fsym(win, tot, S, pp.z);
+      if (lu) s3 = fsym(win, tot, S, pp.w);
     }
   }
   L.pos += tot;
