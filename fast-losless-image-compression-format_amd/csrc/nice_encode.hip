@@ -487,7 +487,7 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 // i-1 can never hit a coded pixel, so it is not tested.)
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
-                                                  uint32_t i) {
+                                                  uint32_t i, const uint32_t* ltab) {
   const uint32_t* b0 = ring + ((s - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b1 = ring + ((s - W - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b2 = ring + ((s - 2u * W) & (CLS_RING - 1)) + tid;
@@ -528,13 +528,27 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
   uint32_t lk = 11u, lt = 0u;
   if (__any(!br && !sd && !l2)) {
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
+    if constexpr (HEAD) {
 #pragma unroll
-    for (int k = 10; k >= 0; --k) {
-      const uint32_t t = xk - refs[k];
-      bool ok = (t & LUMA_MASK) == 0;
-      if constexpr (HEAD) ok = ok && i > 0 && i >= (uint32_t)lr_rows(k) * W + (uint32_t)lr_px(k);
-      lk = ok ? (uint32_t)k : lk;
-      lt = ok ? t : lt;
+      for (int k = 10; k >= 0; --k) {
+        const uint32_t t = xk - refs[k];
+        const bool ok = (t & LUMA_MASK) == 0 && i > 0 && i >= (uint32_t)lr_rows(k) * W + (uint32_t)lr_px(k);
+        lk = ok ? (uint32_t)k : lk;
+        lt = ok ? t : lt;
+      }
+    } else {
+      // first hit = min over k of ((t_k & LUMA_MASK) | k): the mask's lowest
+      // bit is 32 > 10, so a miss keys >= 32 and a hit keys k (one v_and_or
+      // per reference, v_min3 trees, no compare/select chains); the hit's
+      // difference is taken again from the ring through the tile's address
+      // table (ltab[k] = ring index of reference k for thread 0)
+      uint32_t key[11];
+#pragma unroll
+      for (int k = 0; k < 11; ++k) key[k] = ((xk - refs[k]) & LUMA_MASK) | (uint32_t)k;
+      const uint32_t m = min(min(min(min(key[0], key[1]), key[2]), min(min(key[3], key[4]), key[5])),
+                             min(min(min(key[6], key[7]), key[8]), min(key[9], key[10])));
+      lk = min(m, 11u);
+      lt = xk - ring[ltab[m & 15u] + tid];
     }
   }
   const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
@@ -555,6 +569,7 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   __shared__ uint32_t snap[N_BINS];        // hist after the previous tile
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ RecBinTable rbt;
+  __shared__ uint32_t ltab[2][CLS_PPT][16];   // [tile parity][q][luma reference]: ring index for thread 0
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total_work = (uint64_t)a.n_frames * T;
   const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
@@ -562,6 +577,9 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   if (w_begin >= w_end) return;
   const int tid = threadIdx.x, lane = tid & 63;
   rbt_init(rbt, tid);
+  // back distance of luma reference k (code.rs:293-339), for the tile tables
+  const uint32_t lback = tid < 16 * CLS_PPT && (tid & 15) < 11
+                             ? (uint32_t)lr_rows(tid & 15) * a.W + (uint32_t)lr_px(tid & 15) : 0u;
   const uint32_t W = a.W;
   const int64_t N = (int64_t)W * a.H;
   for (int b = tid; b < N_BINS; b += CLS_THREADS) { hist[b] = 0; snap[b] = 0; }
@@ -636,6 +654,11 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       ring[k] = y;
       if (k < CLS_GUARD) ring[CLS_RING + k] = y;
     }
+    // this tile's luma reference table (double-buffered: the previous tile's
+    // readers are past the staging barrier below before it is rewritten)
+    if (tid < 16 * CLS_PPT)
+      ltab[w & 1][tid >> 4][tid & 15] =
+          ((uint32_t)(start + (tid >> 4) * CLS_THREADS) - lback) & (CLS_RING - 1);
     nx.step(1);
     if (w + 1 < w_end) fetch(nx, pf);
     __syncthreads();
@@ -683,9 +706,10 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       const bool coded = (coded_bits >> q) & 1u;
       uint32_t rf;
       if (fast)   // block-uniform: both variants are straight-line code
-        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u);
+        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q]);
       else
-        rf = classify_ring<true>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p));
+        rf = classify_ring<true>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p),
+                                 nullptr);
       rec[q] = coded ? rf : REC_UNCODED;
     }
 #pragma unroll
