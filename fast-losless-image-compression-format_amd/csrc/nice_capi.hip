@@ -897,6 +897,26 @@ int nice_ctx_read_timing(nice_ctx* ctx, double* ms, uint32_t* count) {
   return NICE_OK;
 }
 
+// Test hook: the device heap replay (enc_tables) on n_vec host count vectors
+// of n <= MAX_ALPHABET symbols; aob receives n_vec * n code lengths.
+int nice_test_code_lengths(const uint32_t* counts, int n_vec, int n, uint8_t* aob) {
+  if (n_vec <= 0 || n <= 0 || n > MAX_ALPHABET || !counts || !aob) return NICE_E_ARG;
+  const size_t cb = (size_t)n_vec * n * 4, ab = (size_t)n_vec * n;
+  void *dc = nullptr, *da = nullptr;
+  NICE_HIP(hipMalloc(&dc, cb));
+  if (hipMalloc(&da, ab) != hipSuccess) { (void)hipFree(dc); return NICE_E_HIP; }
+  int rc = NICE_OK;
+  if (hipMemcpy(dc, counts, cb, hipMemcpyHostToDevice) != hipSuccess) rc = NICE_E_HIP;
+  if (!rc) {
+    hipLaunchKernelGGL(enc_code_lengths_test, dim3(n_vec), dim3(64), 0, 0, (const uint32_t*)dc, n, (uint8_t*)da);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(aob, da, ab, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = NICE_E_HIP;
+  }
+  (void)hipFree(dc);
+  (void)hipFree(da);
+  return rc;
+}
+
 const char* nice_phase_name(int phase) {
   return (phase >= 0 && phase < NICE_PHASES) ? kPhaseNames[phase] : "";
 }

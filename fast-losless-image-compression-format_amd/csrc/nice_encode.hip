@@ -867,7 +867,7 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
 #ifdef NICE_PROF_TABLES
   const long long pt0 = clock64();
 #endif
-  if (lane == 0) huffman_merge_tree(h, counts, n);
+  huffman_merge_wave(h, counts, n);
   __syncthreads();
 #ifdef NICE_PROF_TABLES
   const long long pt1 = clock64();
@@ -928,6 +928,24 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
       atomicOr(&a.frame_flags[f], FLAG_LONG);
       atomicOr(&a.frame_flags[a.n_frames], FLAG_LONG);   // any frame of the batch
     }
+  }
+}
+
+// Test hook (nice_test_code_lengths): code lengths of n_vec count vectors of
+// n symbols, one wave each, through the same heap replay as enc_tables.
+__global__ __launch_bounds__(64) void enc_code_lengths_test(const uint32_t* counts, int n, uint8_t* aob) {
+  __shared__ HeapLds h;
+  __shared__ uint32_t c[MAX_ALPHABET];
+  const uint32_t v = blockIdx.x;
+  for (int i = threadIdx.x; i < n; i += 64) c[i] = counts[(uint64_t)v * n + i];
+  for (int i = threadIdx.x; i < 2 * MAX_ALPHABET + 2; i += 64) h.parent[i] = -1;
+  __syncthreads();
+  huffman_merge_wave(h, c, n);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 64) {
+    uint32_t depth = 0;
+    for (int p = h.parent[i]; p >= 0; p = h.parent[p]) ++depth;
+    aob[(uint64_t)v * n + i] = (uint8_t)(1u + depth);
   }
 }
 

@@ -15,95 +15,156 @@
 
 namespace nice {
 
-// One heap slot: count in the high 32 bits would not be enough for very large
-// frames, so keep the full u64 count and a node id side by side.
+// Heap slots hold count << 10 | node id (ids < 2 * MAX_ALPHABET < 1024), so a
+// slot is one 64-bit LDS word and cnt(a) > cnt(b) <=> (a | 1023) > (b | 1023).
 struct HeapLds {
-  unsigned long long cnt[MAX_ALPHABET + 1];
-  int16_t node[MAX_ALPHABET + 1];
+  unsigned long long key[512];
   int16_t parent[2 * MAX_ALPHABET + 2];
   uint8_t aob[MAX_ALPHABET + 1];
   uint16_t order[MAX_ALPHABET + 1];     // symbols in (aob desc, symbol desc) order
 };
+static_assert(2 * MAX_ALPHABET < 1024 && MAX_ALPHABET < 256 + 128, "heap depth <= 8, internal nodes <= level 7");
 
-// std BinaryHeap::sift_up(start, pos): moves up while elem.cnt < parent.cnt.
-__device__ inline void heap_sift_up(HeapLds& h, int start, int pos) {
-  const unsigned long long ec = h.cnt[pos];
-  const int16_t en = h.node[pos];
-  while (pos > start) {
-    const int parent = (pos - 1) >> 1;
-    const unsigned long long pc = h.cnt[parent];
-    if (pc <= ec) break;
-    h.cnt[pos] = pc;
-    h.node[pos] = h.node[parent];
-    pos = parent;
-  }
-  h.cnt[pos] = ec;
-  h.node[pos] = en;
-}
+// ---------------------------------------------------------------------------
+// std BinaryHeap replay on one wave (hfe.rs:63-84; Rust library semantics:
+// push = sift_up(0, len-1); pop = remove the last slot, then
+// sift_down_to_bottom(0) -- the hole walks to a leaf, at every node taking the
+// right child iff cnt(right) <= cnt(left) -- and sift_up of the old last
+// element from there; sift_up moves while cnt(parent) > cnt(elem)).
+//
+// Instead of one lane stepping level by level through LDS, the wave keeps each
+// internal node's walk direction ("pref" bit: 1 = right child) in registers:
+//   * nodes 0..62 (levels 0..5): lane L holds node L's bit (pm), so the whole
+//     top of the tree is one ballot M; lane L also holds the ancestor mask A and
+//     required bits R of level-6 node 63+L, so the lane reached by the walk is
+//     the one with (M & A) == R -- six levels in one compare;
+//   * levels 6..7 (n <= 343: nothing deeper has children): lane L holds the
+//     bits of node 63+L and its two children (P), read once by readlane.
+// The path nodes' contents and siblings are then gathered in one LDS round
+// (lane d = level d), the sift_up stop level is one ballot, the moves are
+// parallel stores, and only the path nodes' pref bits are recomputed (their
+// children are the only ones that changed; plus the parent of the removed
+// last slot).  Bits of leaves and of slots past the end are don't-cares: the
+// walk is cut at the deepest existing node.  Checked against the oracle on
+// 20 000 random count vectors by tools/heap_model.cpp (the same steps as
+// plain loops) before it was written here.
+// ---------------------------------------------------------------------------
+struct WaveHeap {
+  HeapLds& h;
+  uint32_t ln, lvl;              // lane, level of node ln (ln < 63)
+  unsigned long long A, R;       // ancestors / required bits of level-6 node 63 + ln
+  uint32_t pm, P;
+  uint32_t len;                  // wave-uniform
 
-// std BinaryHeap::sift_down_to_bottom(0) followed by sift_up.
-__device__ inline void heap_sift_down_to_bottom(HeapLds& h, int len) {
-  const unsigned long long ec = h.cnt[0];
-  const int16_t en = h.node[0];
-  int pos = 0;
-  int child = 1;
-  while (len >= 2 && child <= len - 2) {
-    const unsigned long long lc = h.cnt[child], rc = h.cnt[child + 1];
-    if (rc <= lc) child += 1;
-    h.cnt[pos] = h.cnt[child];
-    h.node[pos] = h.node[child];
-    pos = child;
-    child = 2 * pos + 1;
-  }
-  if (child == len - 1) {
-    h.cnt[pos] = h.cnt[child];
-    h.node[pos] = h.node[child];
-    pos = child;
-  }
-  h.cnt[pos] = ec;
-  h.node[pos] = en;
-  heap_sift_up(h, 0, pos);
-}
-
-// Serial heap replay by one lane.  counts[] has n entries.  Writes h.parent.
-__device__ inline void huffman_merge_tree(HeapLds& h, const uint32_t* counts, int n) {
-  int len = 0;
-  for (int i = 0; i < n; ++i) {
-    h.cnt[len] = counts[i];
-    h.node[len] = (int16_t)i;
-    ++len;
-    heap_sift_up(h, 0, len - 1);
-  }
-  int next = n;
-  while (len > 2) {
-    // pop #1
-    --len;
-    unsigned long long ac = h.cnt[0];
-    int16_t an = h.node[0];
-    h.cnt[0] = h.cnt[len];
-    h.node[0] = h.node[len];
-    heap_sift_down_to_bottom(h, len);
-    // pop #2
-    --len;
-    unsigned long long bc;
-    int16_t bn;
-    if (len > 0) {
-      bc = h.cnt[0];
-      bn = h.node[0];
-      h.cnt[0] = h.cnt[len];
-      h.node[0] = h.node[len];
-      heap_sift_down_to_bottom(h, len);
-    } else {
-      bc = h.cnt[0];
-      bn = h.node[0];
+  __device__ explicit WaveHeap(HeapLds& hh) : h(hh), ln(threadIdx.x & 63), pm(0), P(0), len(0) {
+    lvl = 31u - (uint32_t)__clz((int)(ln + 1u));
+    A = 0;
+    R = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 6; ++d) {
+      const uint32_t anc = ((64u + ln) >> (6u - d)) - 1u, bit = ((64u + ln) >> (5u - d)) & 1u;
+      A |= 1ull << anc;
+      R |= (unsigned long long)bit << anc;
     }
-    const int16_t id = (int16_t)next++;
-    h.parent[an] = id;
-    h.parent[bn] = id;
-    h.cnt[len] = ac + bc;
-    h.node[len] = id;
-    ++len;
-    heap_sift_up(h, 0, len - 1);
+  }
+  __device__ static bool gt(unsigned long long a, unsigned long long b) { return (a | 1023ull) > (b | 1023ull); }
+
+  // pref bits of the path nodes at levels [lo, hi): node at level d is
+  // (x1 >> (D - d)) - 1 (x1 = deepest path node + 1, at level D), its new bit
+  // is bit d of `bits`
+  __device__ void apply(uint32_t x1, uint32_t D, uint32_t lo, uint32_t hi, unsigned long long bits) {
+    const bool on = ln < 63u && lvl >= lo && lvl < hi && ((x1 >> ((D - lvl) & 31u)) - 1u) == ln;
+    pm = on ? (uint32_t)(bits >> lvl) & 1u : pm;
+    if (hi > 6u) {   // uniform
+      const uint32_t r = (x1 >> (D - 6u)) - 64u;
+      uint32_t q = P;
+      if (lo <= 6u) q = (q & ~1u) | ((uint32_t)(bits >> 6) & 1u);
+      if (hi > 7u && lo <= 7u) {
+        const uint32_t l = 1u + ((x1 >> (D - 7u)) & 1u);
+        q = (q & ~(1u << l)) | (((uint32_t)(bits >> 7) & 1u) << l);
+      }
+      P = ln == r ? q : P;
+    }
+  }
+  __device__ void clear_pref(uint32_t q) {   // uniform node index
+    if (q < 63u) {
+      pm = ln == q ? 0u : pm;
+    } else {
+      const uint32_t D = 31u - (uint32_t)__clz((int)(q + 1u));
+      const uint32_t r = ((q + 1u) >> (D - 6u)) - 64u, t = D - 6u;
+      const uint32_t l = (1u << t) - 1u + ((q + 1u) - ((64u + r) << t));
+      P = ln == r ? (P & ~(1u << l)) : P;
+    }
+  }
+
+  __device__ unsigned long long pop() {
+    const unsigned long long top = h.key[0];
+    const uint32_t e = --len;
+    if (e == 0) return top;
+    const unsigned long long elem = h.key[e];
+    if (!(e & 1u)) clear_pref((e - 1u) >> 1);   // its right child is gone
+    // the walk to the bottom
+    const unsigned long long M = __ballot(pm != 0u);
+    const uint32_t r6 = (uint32_t)__builtin_ctzll(__ballot((M & A) == R));
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)P, (int)r6);
+    const uint32_t l1 = 1u + (s & 1u), l2 = 2u * l1 + 1u + ((s >> l1) & 1u);
+    const uint32_t x1 = ((64u + r6) << 2) + (l2 - 3u);   // level-8 node + 1
+    const uint32_t pd = (x1 >> (8u - min(ln, 8u))) - 1u;   // path node of level ln
+    const uint32_t k = (uint32_t)__popcll(__ballot(ln <= 8u && pd < len)) - 1u;   // bottom level
+    const uint32_t c = (x1 >> (7u - min(ln, 7u))) - 1u;    // its path child
+    const uint32_t c2 = (x1 >> (6u - min(ln, 6u))) - 1u;   // and grandchild
+    const uint32_t sib = (c & 1u) ? c + 1u : c - 1u;
+    const unsigned long long v = h.key[c], v2 = h.key[c2], sv = h.key[sib];
+    // sift_up of elem from the bottom: it rises past level d while cnt(v_d) > cnt(elem)
+    const unsigned long long nb = __ballot(ln < k && !gt(v, elem));
+    const uint32_t j = nb ? 64u - (uint32_t)__clzll(nb) : 0u;
+    if (ln < j) h.key[pd] = v;
+    if (ln == j) h.key[pd] = elem;
+    const unsigned long long nc = ln + 1u < j ? v2 : elem;   // new content of c (ln < j)
+    const bool codd = c & 1u;
+    const uint32_t right = codd ? sib : c;
+    const unsigned long long lv = codd ? nc : sv, rv = codd ? sv : nc;
+    const unsigned long long bits = __ballot(right < len && !gt(rv, lv));
+    apply(x1, 8u, 0u, j, bits);
+    return top;
+  }
+
+  __device__ void push(unsigned long long x) {
+    const uint32_t e = len++;
+    if (e == 0) { h.key[0] = x; return; }
+    const uint32_t x1 = e + 1u;
+    const uint32_t D = 31u - (uint32_t)__clz((int)x1);
+    const uint32_t ad = (x1 >> (D - min(ln, D))) - 1u;          // path node of level ln
+    const uint32_t c = (x1 >> (D - min(ln + 1u, D))) - 1u;      // its path child
+    const uint32_t sib = (c & 1u) ? c + 1u : c - 1u;
+    const unsigned long long old = h.key[ad], sv = h.key[sib];
+    const unsigned long long nb = __ballot(ln < D && !gt(old, x));
+    const uint32_t j = nb ? 64u - (uint32_t)__clzll(nb) : 0u;   // x's final level
+    if (ln == j) h.key[ad] = x;
+    if (ln >= j && ln < D) h.key[c] = old;                       // shifted one level down
+    const uint32_t lo = j ? j - 1u : 0u;
+    const unsigned long long nc = ln + 1u == j ? x : old;        // new content of c (ln >= lo)
+    const bool codd = c & 1u;
+    const uint32_t right = codd ? sib : c;
+    const unsigned long long lv = codd ? nc : sv, rv = codd ? sv : nc;
+    const unsigned long long bits = __ballot(right < len && !gt(rv, lv));
+    apply(x1, D, lo, D, bits);
+  }
+};
+
+// hfe.rs:63-84 on one wave.  counts[] has n entries.  Writes h.parent.
+__device__ inline void huffman_merge_wave(HeapLds& h, const uint32_t* counts, int n) {
+  WaveHeap q(h);
+  for (int i = 0; i < n; ++i) q.push(((unsigned long long)counts[i] << 10) | (unsigned long long)i);
+  uint32_t next = (uint32_t)n;
+  while (q.len > 2) {
+    const unsigned long long a = q.pop(), b = q.pop();
+    if (q.ln == 0) {
+      h.parent[a & 1023u] = (int16_t)next;
+      h.parent[b & 1023u] = (int16_t)next;
+    }
+    q.push((((a >> 10) + (b >> 10)) << 10) | next);
+    ++next;
   }
 }
 

@@ -72,6 +72,7 @@ constexpr uint32_t DEC_PARSE_THREADS = 512;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring
 __global__ void enc_tailruns(EncArgs a);
 __global__ void enc_tables(EncArgs a);
+__global__ void enc_code_lengths_test(const uint32_t* counts, int n, uint8_t* aob);
 __global__ void enc_header(EncArgs a);
 __global__ void enc_tilebits(EncArgs a);
 __global__ void enc_tilebits_hist(EncArgs a);
