@@ -872,52 +872,121 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
 #ifdef NICE_PROF_TABLES
   const long long pt1 = clock64();
 #endif
-  // aob = 1 + number of merged ancestors (u8 wrapping, hfe.rs:79-82)
+  // aob = 1 + number of merged ancestors (u8 wrapping, hfe.rs:79-82); the
+  // lane's symbols' parent chains are walked together (independent loads)
+  constexpr int SPL = (MAX_ALPHABET + 63) / 64;
+  __shared__ uint32_t lvl_n[256], lvl_run[256];
+  __shared__ unsigned long long lvl_cur[256];
+  for (int b = lane; b < 256; b += 64) { lvl_n[b] = 0; lvl_run[b] = 0; }
+  int pp[SPL];
+  uint32_t ab[SPL];
+#pragma unroll
+  for (int q = 0; q < SPL; ++q) {
+    const int i = lane + 64 * q;
+    pp[q] = i < n ? h.parent[i] : -1;
+    ab[q] = 1u;
+  }
+  while (true) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+      if (pp[q] >= 0) {
+        ++ab[q];
+        pp[q] = h.parent[pp[q]];
+        any = true;
+      }
+    }
+    if (!__any(any)) break;
+  }
   uint32_t my_max = 0, my_emit_max = 0;
-  for (int i = lane; i < n; i += 64) {
-    uint32_t depth = 0;
-    for (int p = h.parent[i]; p >= 0; p = h.parent[p]) ++depth;
-    const uint8_t aob = (uint8_t)(1u + depth);
-    h.aob[i] = aob;
-    my_max = max(my_max, (uint32_t)aob);
-    if (counts[i]) my_emit_max = max(my_emit_max, (uint32_t)aob);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < SPL; ++q) {
+    const int i = lane + 64 * q;
+    ab[q] &= 255u;
+    if (i < n) {
+      my_max = max(my_max, ab[q]);
+      if (counts[i]) my_emit_max = max(my_emit_max, ab[q]);
+      atomicAdd(&lvl_n[ab[q]], 1u);
+    }
+  }
+  // canonical order (hfe.rs:264-270): lengths descending, then symbols
+  // descending.  t = a symbol's place within its length = the symbols above it
+  // with the same length: chunks of 64 from the top, one ballot per distinct
+  // length in the chunk, running totals per length in LDS
+  uint32_t t[SPL];
+#pragma unroll
+  for (int q = SPL - 1; q >= 0; --q) {
+    const bool valid = lane + 64 * q < n;
+    unsigned long long rem = __ballot(valid);
+    t[q] = 0;
+    while (rem) {
+      const uint32_t av = (uint32_t)__builtin_amdgcn_readlane((int)ab[q], (int)__builtin_ctzll(rem));
+      const bool mine = valid && ab[q] == av;
+      const unsigned long long m = __ballot(mine);
+      const uint32_t run = lvl_run[av];
+      if (mine) t[q] = run + (uint32_t)__popcll(lane < 63 ? m >> (lane + 1) : 0ull);
+      if (lane == 0) lvl_run[av] = run + (uint32_t)__popcll(m);
+      rem &= ~m;
+    }
+  }
+  // hfe.rs:271-290 (usize wrapping): the running code `cur` steps by one per
+  // symbol within a length (not after a length-0 symbol: `prev > 0`) and is
+  // shifted right by the length drop at each new length, so only its value at
+  // each present length's first symbol is serial: one scalar pass over the
+  // present lengths (ballots of the length histogram, bin a = lane a & 63 of
+  // word a >> 6)
+  __syncthreads();
+  uint32_t ln_cnt[4];
+  unsigned long long pres[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ln_cnt[r] = lvl_n[64 * r + lane];
+    pres[r] = __ballot(ln_cnt[r] != 0);
+  }
+  {
+    unsigned long long cur = 0;
+    uint32_t prev = 0;
+    bool first = true;
+#pragma unroll
+    for (int r = 3; r >= 0; --r) {
+      unsigned long long pm = pres[r];
+      while (pm) {
+        const uint32_t l = 63u - (uint32_t)__clzll(pm);
+        pm &= ~(1ull << l);
+        const uint32_t av = 64u * r + l;
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)ln_cnt[r], (int)l);
+        if (!first) cur = (cur >> ((prev - av) & 63u)) + 1ull;   // prev > av >= 0: the shift, then prev > 0
+        first = false;
+        if (lane == 0) lvl_cur[av] = cur;
+        cur += av ? (unsigned long long)(c - 1u) : 0ull;
+        prev = av;
+      }
+    }
   }
   __syncthreads();
-  // order = symbols sorted by (aob desc, symbol desc): rank by counting.
-  for (int i = lane; i < n; i += 64) {
-    const uint8_t ai = h.aob[i];
-    int rank = 0;
-    for (int j = 0; j < n; ++j) {
-      const uint8_t aj = h.aob[j];
-      rank += (aj > ai) || (aj == ai && j > i);
+#ifdef NICE_PROF_TABLES
+  const long long pt2 = clock64();
+#endif
+#pragma unroll
+  for (int q = 0; q < SPL; ++q) {
+    const int i = lane + 64 * q;
+    if (i < n) {
+      const uint32_t av = ab[q];
+      const unsigned long long cur = lvl_cur[av] + (av ? t[q] : 0u);
+      const unsigned long long code = (1ull << (av & 63u)) - cur - 1ull;
+      const uint64_t e = (uint64_t)f * N_BINS + sb + i;
+      a.tbl_len8[e] = (uint8_t)av;
+      a.tbl_code[e] = (uint32_t)code;
+      a.tbl[e] = (av <= FAST_MAX_CODE_BITS) ? (uint32_t)((code << 5) | av) : 0u;
     }
-    h.order[rank] = (uint16_t)i;
   }
   // wave max
   for (int o = 32; o > 0; o >>= 1) {
     my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, o));
     my_emit_max = max(my_emit_max, (uint32_t)__shfl_xor((int)my_emit_max, o));
   }
-  __syncthreads();
-#ifdef NICE_PROF_TABLES
-  const long long pt2 = clock64();
-#endif
   if (lane == 0) {
-    // hfe.rs:271-290 with usize wrapping arithmetic
-    unsigned long long cur = 0;
-    uint8_t prev = 0;
-    for (int k = 0; k < n; ++k) {
-      const int sym = h.order[k];
-      const uint8_t aob = h.aob[sym];
-      if (aob < prev) cur >>= ((uint8_t)(prev - aob)) & 63u;
-      if (prev > 0) cur += 1;
-      const unsigned long long code = (1ull << (aob & 63u)) - cur - 1ull;
-      const uint64_t e = (uint64_t)f * N_BINS + sb + sym;
-      a.tbl_len8[e] = aob;
-      a.tbl_code[e] = (uint32_t)code;
-      a.tbl[e] = (aob <= FAST_MAX_CODE_BITS) ? (uint32_t)((code << 5) | aob) : 0u;
-      prev = aob;
-    }
     a.stream_max[(uint64_t)f * N_STREAMS + s] = (uint8_t)my_max;
 #ifdef NICE_PROF_TABLES
     const long long pt3 = clock64();

@@ -20,8 +20,6 @@ namespace nice {
 struct HeapLds {
   unsigned long long key[512];
   int16_t parent[2 * MAX_ALPHABET + 2];
-  uint8_t aob[MAX_ALPHABET + 1];
-  uint16_t order[MAX_ALPHABET + 1];     // symbols in (aob desc, symbol desc) order
 };
 static_assert(2 * MAX_ALPHABET < 1024 && MAX_ALPHABET < 256 + 128, "heap depth <= 8, internal nodes <= level 7");
 
