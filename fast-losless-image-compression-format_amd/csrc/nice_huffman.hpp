@@ -15,8 +15,9 @@
 
 namespace nice {
 
-// Heap slots hold count << 10 | node id (ids < 2 * MAX_ALPHABET < 1024), so a
-// slot is one 64-bit LDS word and cnt(a) > cnt(b) <=> (a | 1023) > (b | 1023).
+// Heap slots hold count << 32 | node id: one 64-bit LDS word, compared on the
+// high word (a stream's total count is at most 3 symbols per pixel -- SC_RGB
+// -- and the boundary caps frames at 2^30 pixels, so every sum fits 32 bits).
 struct HeapLds {
   unsigned long long key[512];
   int16_t parent[2 * MAX_ALPHABET + 2];
@@ -65,7 +66,9 @@ struct WaveHeap {
       R |= (unsigned long long)bit << anc;
     }
   }
-  __device__ static bool gt(unsigned long long a, unsigned long long b) { return (a | 1023ull) > (b | 1023ull); }
+  __device__ static bool gt(unsigned long long a, unsigned long long b) {
+    return (uint32_t)(a >> 32) > (uint32_t)(b >> 32);
+  }
 
   // pref bits of the path nodes at levels [lo, hi): node at level d is
   // (x1 >> (D - d)) - 1 (x1 = deepest path node + 1, at level D), its new bit
@@ -73,26 +76,19 @@ struct WaveHeap {
   __device__ void apply(uint32_t x1, uint32_t D, uint32_t lo, uint32_t hi, unsigned long long bits) {
     const bool on = ln < 63u && lvl >= lo && lvl < hi && ((x1 >> ((D - lvl) & 31u)) - 1u) == ln;
     pm = on ? (uint32_t)(bits >> lvl) & 1u : pm;
-    if (hi > 6u) {   // uniform
-      const uint32_t r = (x1 >> (D - 6u)) - 64u;
-      uint32_t q = P;
-      if (lo <= 6u) q = (q & ~1u) | ((uint32_t)(bits >> 6) & 1u);
-      if (hi > 7u && lo <= 7u) {
-        const uint32_t l = 1u + ((x1 >> (D - 7u)) & 1u);
-        q = (q & ~(1u << l)) | (((uint32_t)(bits >> 7) & 1u) << l);
-      }
-      P = ln == r ? q : P;
-    }
+    // levels 6 and 7 (scalar masks, no branches): lane r, bit 0 and bit l
+    const uint32_t r = (x1 >> ((D - 6u) & 31u)) - 64u;
+    const uint32_t l = 1u + ((x1 >> ((D - 7u) & 31u)) & 1u);
+    const uint32_t m6 = (lo <= 6u && hi > 6u) ? 1u : 0u, m7 = (lo <= 7u && hi > 7u) ? (1u << l) : 0u;
+    const uint32_t nb = ((uint32_t)(bits >> 6) & 1u) | ((((uint32_t)(bits >> 7)) & 1u) << l);
+    P = ln == r ? (P & ~(m6 | m7)) | (nb & (m6 | m7)) : P;
   }
-  __device__ void clear_pref(uint32_t q) {   // uniform node index
-    if (q < 63u) {
-      pm = ln == q ? 0u : pm;
-    } else {
-      const uint32_t D = 31u - (uint32_t)__clz((int)(q + 1u));
-      const uint32_t r = ((q + 1u) >> (D - 6u)) - 64u, t = D - 6u;
-      const uint32_t l = (1u << t) - 1u + ((q + 1u) - ((64u + r) << t));
-      P = ln == r ? (P & ~(1u << l)) : P;
-    }
+  __device__ void clear_pref(uint32_t q, bool go) {   // uniform node index (levels <= 7), no branches
+    pm = (go && ln == q) ? 0u : pm;
+    const uint32_t D = 31u - (uint32_t)__clz((int)(q + 1u));
+    const uint32_t r = ((q + 1u) >> ((D - 6u) & 31u)) - 64u;
+    const uint32_t l = (D == 7u) ? 1u + ((q + 1u) & 1u) : 0u;
+    P = (go && q >= 63u && ln == r) ? (P & ~(1u << l)) : P;
   }
 
   __device__ unsigned long long pop() {
@@ -100,7 +96,7 @@ struct WaveHeap {
     const uint32_t e = --len;
     if (e == 0) return top;
     const unsigned long long elem = h.key[e];
-    if (!(e & 1u)) clear_pref((e - 1u) >> 1);   // its right child is gone
+    clear_pref((e - 1u) >> 1, !(e & 1u));   // a right child is gone
     // the walk to the bottom
     const unsigned long long M = __ballot(pm != 0u);
     const uint32_t r6 = (uint32_t)__builtin_ctzll(__ballot((M & A) == R));
@@ -116,8 +112,7 @@ struct WaveHeap {
     // sift_up of elem from the bottom: it rises past level d while cnt(v_d) > cnt(elem)
     const unsigned long long nb = __ballot(ln < k && !gt(v, elem));
     const uint32_t j = nb ? 64u - (uint32_t)__clzll(nb) : 0u;
-    if (ln < j) h.key[pd] = v;
-    if (ln == j) h.key[pd] = elem;
+    if (ln <= j) h.key[pd] = ln < j ? v : elem;
     const unsigned long long nc = ln + 1u < j ? v2 : elem;   // new content of c (ln < j)
     const bool codd = c & 1u;
     const uint32_t right = codd ? sib : c;
@@ -153,15 +148,15 @@ struct WaveHeap {
 // hfe.rs:63-84 on one wave.  counts[] has n entries.  Writes h.parent.
 __device__ inline void huffman_merge_wave(HeapLds& h, const uint32_t* counts, int n) {
   WaveHeap q(h);
-  for (int i = 0; i < n; ++i) q.push(((unsigned long long)counts[i] << 10) | (unsigned long long)i);
+  for (int i = 0; i < n; ++i) q.push(((unsigned long long)counts[i] << 32) | (unsigned long long)i);
   uint32_t next = (uint32_t)n;
   while (q.len > 2) {
     const unsigned long long a = q.pop(), b = q.pop();
     if (q.ln == 0) {
-      h.parent[a & 1023u] = (int16_t)next;
-      h.parent[b & 1023u] = (int16_t)next;
+      h.parent[(uint32_t)a] = (int16_t)next;
+      h.parent[(uint32_t)b] = (int16_t)next;
     }
-    q.push((((a >> 10) + (b >> 10)) << 10) | next);
+    q.push((((a >> 32) + (b >> 32)) << 32) | next);
     ++next;
   }
 }

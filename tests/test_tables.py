@@ -1,7 +1,9 @@
 """Device Huffman code lengths (enc_tables' wave-parallel BinaryHeap replay,
 nice_huffman.hpp) against the oracle's literal replay of hfe.rs:58-87 + std
 BinaryHeap on random count vectors -- tie-heavy, sparse and wide counts, every
-stream size of the format (code.rs:91-116) plus tiny heaps."""
+stream size of the format (code.rs:91-116) plus tiny heaps.  Count totals
+stay below 2^31, as a frame's do (the boundary caps frames at 2^30 pixels, at
+most 3 symbols per pixel per stream), matching the device's 32-bit sums."""
 import ctypes
 
 import numpy as np
@@ -22,12 +24,12 @@ def _vectors(n, k, rng):
             c = np.where(rng.integers(0, 3, n) == 0, 0, rng.integers(0, 100000, n))
         elif mode == 3:
             c = np.where(rng.integers(0, 2, n) == 0, 5, 7)
-        elif mode == 4:
-            c = rng.integers(0, 1 << 31, n)
+        elif mode == 4:   # wide counts; a stream total below 2^31
+            c = rng.integers(0, (1 << 31) // n, n)
         else:   # Fibonacci-like: deep trees
             f = [1, 1]
             while len(f) < n:
-                f.append(min(f[-1] + f[-2], 1 << 30))
+                f.append(min(f[-1] + f[-2], (1 << 31) // n))
             c = np.array(f[:n])[rng.permutation(n)]
         out.append(c.astype(np.uint32))
     return np.stack(out)
