@@ -1146,7 +1146,14 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t f = blockIdx.y, j = blockIdx.x * DEC_PLACE_WAVES + (threadIdx.x >> 6);   // grid (slices / waves, frames)
+  // grid (slices / waves, frames), XCD-aware: consecutive logical blocks are
+  // dealt to one XCD (blocks b and b + 8 share one; bijective remap, guide T1),
+  // so the two blocks whose slices share each 128-byte event line (8 slices'
+  // 16-byte quads, interleaved per parse wave) read it through one L2
+  const uint32_t nbx = gridDim.x, nwg = nbx * gridDim.y, lin = blockIdx.y * nbx + blockIdx.x;
+  const uint32_t xq = nwg / 8u, xr = nwg % 8u, xcd = lin % 8u;
+  const uint32_t lg = (xcd < xr ? xcd * (xq + 1u) : xr * (xq + 1u) + (xcd - xr) * xq) + lin / 8u;
+  const uint32_t f = lg / nbx, j = (lg % nbx) * DEC_PLACE_WAVES + (threadIdx.x >> 6);
   if (a.status[f] != 0) return;
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
