@@ -214,6 +214,20 @@ __device__ __forceinline__ uint32_t rec_bins(const RecBinTable& t, uint32_t rec,
   return rb.x >> 8;
 }
 
+// Each mode's identifying stream and symbols per pixel (code.rs:191-366):
+// BACK_REF one SC_BACK_REF symbol, RGB three SC_RGB, LUMA one
+// SC_LUMA_BACK_REF, SMALL_DIFF one SC_SMALL_DIFF1, LUMA2 one
+// SC_LUMA_BASE_DIFF2 -- so a mode's prefix count is its stream's total
+// divided by that number, and the classify pass does not count prefixes.
+__device__ __forceinline__ bool mode_id_bin(int k, int b) {
+  const int lo = k == P_BACK_REF ? BIN_BACK_REF : k == P_RGB ? 0 : k == P_LUMA ? BIN_LUMA_REF
+               : k == P_SMALL_DIFF ? BIN_SMALL_DIFF : BIN_LUMA2_BASE;
+  const int n = k == P_BACK_REF ? N_BINS - BIN_BACK_REF : k == P_RGB ? 256 : k == P_LUMA ? 11
+              : k == P_SMALL_DIFF ? 343 : 64;
+  return b >= lo && b < lo + n;
+}
+__device__ __forceinline__ uint32_t mode_id_syms(int k) { return k == P_RGB ? 3u : 1u; }
+
 // Work item -> (frame, tile) without a 64-bit division per tile (one at the
 // start; the scalar division sequence is ~100 instructions).
 struct TileIter {
@@ -717,19 +731,9 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       const int p = q * CLS_THREADS + tid;
       const bool coded = (coded_bits >> q) & 1u;
       if (p < count) recs[p] = rec[q];
-      {
-        // mode prefixes counted per wave (ballots; lanes 0..4 add them).
-        // Measured: per-lane packed counters summed by DPP once per tile were
-        // 8 % slower
-        const uint32_t m = rec[q] & 7u;   // REC_UNCODED (7) for run members
-        uint32_t pc = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 5; ++k) {
-          const uint32_t c = (uint32_t)__popcll(__ballot(m == k));
-          pc = (uint32_t)lane == k ? c : pc;
-        }
-        if (lane < 5 && pc) atomicAdd(&hist[BIN_PREFIX + lane], pc);
-      }
+      // the mode prefixes (bins BIN_PREFIX + 0..4) are not counted here: each
+      // mode emits a fixed number of symbols into one stream of its own, so
+      // enc_tables and enc_tilebits_hist derive them (mode_prefix_count)
       {
         // payload symbols: four unconditional LDS adds, absent ones into this
         // lane's discard slot (no divergent branches)
@@ -863,6 +867,21 @@ __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
   const int lane = threadIdx.x;
   for (int i = lane; i < n; i += 64) counts[i] = a.hist[(uint64_t)f * N_BINS + sb + i];
   for (int i = lane; i < 2 * MAX_ALPHABET + 2; i += 64) h.parent[i] = -1;
+  if (s == S_PREFIX) {   // the mode prefixes from their payload streams (every classify variant)
+    __syncthreads();
+    const uint32_t* hf = a.hist + (uint64_t)f * N_BINS;
+    uint32_t c[5] = {0, 0, 0, 0, 0};
+    for (int b = lane; b < N_BINS; b += 64) {
+      const uint32_t v = hf[b];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) c[k] += mode_id_bin(k, b) ? v : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      for (int o = 32; o > 0; o >>= 1) c[k] += (uint32_t)__shfl_xor((int)c[k], o);
+      if (lane == k) counts[k] = c[k] / mode_id_syms(k);
+    }
+  }
   __syncthreads();
 #ifdef NICE_PROF_TABLES
   const long long pt0 = clock64();
@@ -1342,7 +1361,7 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
   __shared__ uint32_t lens_all[4][2 * TH_WORDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t* lens = lens_all[wid];
-  uint32_t cur_f = 0xFFFFFFFFu;
+  uint32_t cur_f = 0xFFFFFFFFu, prefix_len_rgb = 0;
   uint64_t t0, t1;
   tile_range(a, t0, t1);
   TileIter it(a, t0 + wid);
@@ -1351,24 +1370,39 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
     const uint32_t f = it.f;
     if (f != cur_f) {
       __builtin_amdgcn_wave_barrier();
-      for (int b = lane; b < (int)(2 * TH_WORDS); b += 64)
-        lens[b] = b < N_BINS ? (uint32_t)a.tbl_len8[(uint64_t)f * N_BINS + b] : 0u;
+      // the mode prefixes are not in the tile counts: each mode's prefix length
+      // rides on the bins of its identifying stream (RGB: once per 3 symbols)
+      const uint8_t* l8 = a.tbl_len8 + (uint64_t)f * N_BINS;
+      uint32_t pl[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) pl[k] = l8[BIN_PREFIX + k];
+      prefix_len_rgb = pl[P_RGB];
+      for (int b = lane; b < (int)(2 * TH_WORDS); b += 64) {
+        uint32_t v = b < N_BINS ? (uint32_t)l8[b] : 0u;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v += (k != P_RGB && mode_id_bin(k, b)) ? pl[k] : 0u;
+        lens[b] = v;
+      }
       cur_f = f;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
     const uint32_t* th = a.tile_hist + t * TH_WORDS;
-    uint32_t acc = 0;
+    uint32_t acc = 0, rgb = 0;
 #pragma unroll
     for (int k0 = 0; k0 < (int)TH_WORDS; k0 += 64) {
       const int k = k0 + lane;
       if (k < (int)TH_WORDS) {
         const uint32_t v = th[k];
         acc += (v & 0xFFFFu) * lens[2 * k] + (v >> 16) * lens[2 * k + 1];
+        if (2 * k < 256) rgb += (v & 0xFFFFu) + (v >> 16);   // SC_RGB symbols: 3 per RGB pixel
       }
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rgb += __shfl_xor(rgb, o);
     if (lane == 0) {
+      acc += rgb / 3u * prefix_len_rgb;
       const uint32_t last = a.tile_last[t];
       if (last != NONE) {
         const uint64_t run = (uint64_t)a.tile_next[t] - last - 1;
