@@ -423,12 +423,7 @@ __device__ __forceinline__ void enc_classify_body(const EncArgs& a) {
           }
         }
       }
-      // mode prefix: aggregate per wave (5 values, heavy contention otherwise)
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        const unsigned long long bal = __ballot(coded && (rec & 7u) == (uint32_t)v);
-        if (lane == v && bal) atomicAdd(&hist[BIN_PREFIX + v], (uint32_t)__popcll(bal));
-      }
+      // mode prefixes: derived by enc_tables from the payload streams (mode_id_bin)
     }
   }
   __syncthreads();
