@@ -121,25 +121,29 @@ __device__ __forceinline__ int next_coded_local(const uint32_t* mask, int p) {
 // K1: classify + histogram + per-pixel symbol records.
 //
 // Record (one u32 per pixel, raster order): bits 0..2 the mode prefix
-// (P_BACK_REF .. P_LUMA2) or REC_UNCODED for a run member; bits 3.. the payload:
-//   BACK_REF  k (3)                 SMALL_DIFF  index 0..342 (9)
-//   LUMA2     g+32 (6), r+16 (5), b+16 (5)
-//   LUMA      k (4), g+32 (6), r+16 (5), b+16 (5)
-//   RGB       r, g, b residuals (8 each)
+// (P_BACK_REF .. P_LUMA2) or REC_UNCODED for a run member; bits 3.. the payload,
+// laid out as the classify arithmetic produces it (the spread/luma-space
+// fields at 10-bit spacing, masked and shifted once):
+//   BACK_REF  k (3) at 3            SMALL_DIFF  index 0..342 (9) at 3
+//   LUMA2     r+16 (5) at 3, g+32 (6) at 13, b+16 (5) at 23
+//   LUMA      k (4) at 3, r+16 (5) at 7, g+32 (6) at 17, b+16 (5) at 27
+//   RGB       r, g, b residuals (8 each) at 3, 13, 23
 // ---------------------------------------------------------------------------
 constexpr uint32_t REC_UNCODED = 7u;
+// the luma payload fields of Y(X) - Y(ref) (r: bits 0-4, g: 10-15, b: 20-24)
+constexpr uint32_t LUMA_FIELDS = 0x1Fu | (0x3Fu << 10) | (0x1Fu << 20);
 
 __device__ __forceinline__ uint32_t rec_from_syms(const PixSyms& s) {
   switch (s.mode) {
     case P_BACK_REF: return P_BACK_REF | ((s.b[0] - BIN_BACK_REF) << 3);
     case P_SMALL_DIFF: return P_SMALL_DIFF | ((s.b[0] - BIN_SMALL_DIFF) << 3);
     case P_LUMA2:
-      return P_LUMA2 | ((s.b[0] - BIN_LUMA2_BASE) << 3) | ((s.b[1] - BIN_LUMA2_R) << 9) |
-             ((s.b[2] - BIN_LUMA2_B) << 14);
+      return P_LUMA2 | ((s.b[0] - BIN_LUMA2_BASE) << 13) | ((s.b[1] - BIN_LUMA2_R) << 3) |
+             ((s.b[2] - BIN_LUMA2_B) << 23);
     case P_LUMA:
-      return P_LUMA | ((s.b[0] - BIN_LUMA_REF) << 3) | ((s.b[1] - BIN_LUMA_BASE) << 7) |
-             ((s.b[2] - BIN_LUMA_OTHER) << 13) | ((s.b[3] - BIN_LUMA_OTHER) << 18);
-    default: return P_RGB | (s.b[0] << 3) | (s.b[1] << 11) | (s.b[2] << 19);
+      return P_LUMA | ((s.b[0] - BIN_LUMA_REF) << 3) | ((s.b[1] - BIN_LUMA_BASE) << 17) |
+             ((s.b[2] - BIN_LUMA_OTHER) << 7) | ((s.b[3] - BIN_LUMA_OTHER) << 27);
+    default: return P_RGB | (s.b[0] << 3) | (s.b[1] << 13) | (s.b[2] << 23);
   }
 }
 
@@ -147,10 +151,10 @@ __device__ __forceinline__ uint32_t rec_from_syms(const PixSyms& s) {
 // (record bits 0..2), payload k is bits [shift, shift+width) of the record plus
 // a histogram base, all looked up in packed constants (no per-mode control flow).
 //   m:        0 BACK_REF   1 RGB        2 LUMA        3 SMALL_DIFF  4 LUMA2
-//   k = 0     847+[3,3)    0+[3,8)      365+[3,4)     376+[3,9)     719+[3,6)
-//   k = 1     -            0+[11,8)     269+[7,6)     -             783+[9,5)
-//   k = 2     -            0+[19,8)     333+[13,5)    -             815+[14,5)
-//   k = 3     -            -            333+[18,5)    -             -
+//   k = 0     847+[3,3)    0+[3,8)      365+[3,4)     376+[3,9)     719+[13,6)
+//   k = 1     -            0+[13,8)     269+[17,6)    -             783+[3,5)
+//   k = 2     -            0+[23,8)     333+[7,5)     -             815+[23,5)
+//   k = 3     -            -            333+[27,5)    -             -
 constexpr unsigned long long rb_pack(int a0, int a1, int a2, int a3, int a4, int bits) {
   return (unsigned long long)a0 | ((unsigned long long)a1 << bits) | ((unsigned long long)a2 << (2 * bits)) |
          ((unsigned long long)a3 << (3 * bits)) | ((unsigned long long)a4 << (4 * bits));
@@ -162,10 +166,10 @@ constexpr unsigned long long RB_BASE[4] = {
     rb_pack(0, 0, BIN_LUMA_OTHER, 0, BIN_LUMA2_B, 10),
     rb_pack(0, 0, BIN_LUMA_OTHER, 0, 0, 10)};
 constexpr unsigned long long RB_FIELD[4] = {
-    rb_pack(3 | 3 << 5, 3 | 8 << 5, 3 | 4 << 5, 3 | 9 << 5, 3 | 6 << 5, 10),
-    rb_pack(0, 11 | 8 << 5, 7 | 6 << 5, 0, 9 | 5 << 5, 10),
-    rb_pack(0, 19 | 8 << 5, 13 | 5 << 5, 0, 14 | 5 << 5, 10),
-    rb_pack(0, 0, 18 | 5 << 5, 0, 0, 10)};
+    rb_pack(3 | 3 << 5, 3 | 8 << 5, 3 | 4 << 5, 3 | 9 << 5, 13 | 6 << 5, 10),
+    rb_pack(0, 13 | 8 << 5, 17 | 6 << 5, 0, 3 | 5 << 5, 10),
+    rb_pack(0, 23 | 8 << 5, 7 | 5 << 5, 0, 23 | 5 << 5, 10),
+    rb_pack(0, 0, 27 | 5 << 5, 0, 0, 10)};
 constexpr uint32_t RB_N = 1u | 3u << 3 | 4u << 6 | 1u << 9 | 3u << 12;   // payload count, 3 bits per mode
 __device__ __forceinline__ uint32_t rb_bin(uint32_t rec, uint32_t m, int k) {
   const uint32_t base = (uint32_t)(RB_BASE[k] >> (10u * m)) & 0x3FFu;
@@ -293,10 +297,9 @@ __device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col, ui
   const uint32_t r = X + K3(256u) - (has_left ? pred : 0u);
   const uint32_t rec_br = P_BACK_REF | (bk << 3);
   const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
-  const uint32_t rec_l2 = P_LUMA2 | (((t2 >> 10) & 63u) << 3) | ((t2 & 31u) << 9) | (((t2 >> 20) & 31u) << 14);
-  const uint32_t rec_lu = P_LUMA | (lk << 3) | (((lt >> 10) & 63u) << 7) | ((lt & 31u) << 13) |
-                          (((lt >> 20) & 31u) << 18);
-  const uint32_t rec_rgb = P_RGB | ((r & 255u) << 3) | (((r >> 10) & 255u) << 11) | (((r >> 20) & 255u) << 19);
+  const uint32_t rec_l2 = P_LUMA2 | ((t2 & LUMA_FIELDS) << 3);
+  const uint32_t rec_lu = P_LUMA | (lk << 3) | ((lt & LUMA_FIELDS) << 7);
+  const uint32_t rec_rgb = P_RGB | ((r & K3(0xFFu)) << 3);
   return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
 }
 
@@ -468,8 +471,9 @@ __device__ __forceinline__ uint32_t y_from_rgba(uint32_t v) {
   return (s + K3(256u) - (g | (g << 20))) & K3(0xFFu);
 }
 __device__ __forceinline__ uint32_t rgb_from_y(uint32_t y) {
+  // g | g << 20 as one 24-bit multiply-add (v_bfe + v_mad_u32_u24 + v_and)
   const uint32_t g = (y >> 10) & 0xFFu;
-  return (y + (g | (g << 20))) & K3(0xFFu);
+  return (y + __umul24(g, 0x100001u)) & K3(0xFFu);
 }
 
 struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W + px)
@@ -529,7 +533,7 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
   const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
   // luma2 against the prediction (code.rs:252-292)
   const uint32_t pg = (pred >> 10) & 0xFFu;
-  const uint32_t py = (pred + K3(256u) - (pg | (pg << 20))) & K3(0xFFu);
+  const uint32_t py = (uint32_t)(__mul24((int)pg, -0x100001) + (int)(pred + K3(256u))) & K3(0xFFu);
   const uint32_t xk = X + LUMA_KY;
   const uint32_t t2 = xk - py;
   const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
@@ -563,12 +567,11 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
   const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
   const uint32_t rec_br = P_BACK_REF | (bk << 3);
   const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
-  // LUMA2 and LUMA share the g | r << 6 | b << 11 field layout (LUMA: after its 4-bit reference)
-  const uint32_t ts = l2 ? t2 : lt;
-  const uint32_t lf = ((ts >> 10) & 63u) | ((ts & 31u) << 6) | (((ts >> 20) & 31u) << 11);
+  // LUMA2 and LUMA keep the luma-space fields in place (LUMA: after its 4-bit reference)
+  const uint32_t lf = (l2 ? t2 : lt) & LUMA_FIELDS;
   const uint32_t rec_l2 = P_LUMA2 | (lf << 3);
   const uint32_t rec_lu = P_LUMA | (lk << 3) | (lf << 7);
-  const uint32_t rec_rgb = P_RGB | ((r & 255u) << 3) | (((r >> 10) & 255u) << 11) | (((r >> 20) & 255u) << 19);
+  const uint32_t rec_rgb = P_RGB | ((r & K3(0xFFu)) << 3);
   return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
 }
 
