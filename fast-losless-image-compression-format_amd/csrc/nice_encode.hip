@@ -1511,20 +1511,18 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
       tile_bits += ws;
     }
     if (Q.nb) {
-      const uint32_t pos = wbase + x - Q.nb;
-      uint64_t acc = 0;
-      uint32_t nacc = pos & 31u, wi = pos >> 5;
-      // n <= 32 bits of val (0 when n == 0).  Branch-free: the top word is OR-ed
-      // into LDS on every put (0 while it is not full) -- a divergent flush
-      // branch per code cost more than the extra LDS OR.
+      uint32_t pp = wbase + x - Q.nb;   // the lane's next bit in the tile
+      // n <= 32 bits of val (0 when n == 0) at bit pp, MSB-first: one 64-bit
+      // shift places them across words pp >> 5 and pp >> 5 + 1, both OR-ed
+      // into LDS (words shared with neighbouring lanes).  No accumulator
+      // carried from put to put, so a lane's puts are independent (measured:
+      // the accumulator version's flush selects were ~14 VALU per put).
       auto put_n = [&](uint32_t val, uint32_t n) {
-        acc |= (uint64_t)val << ((64u - nacc - n) & 63u);
-        nacc += n;
-        const bool fl = nacc >= 32u;
-        atomicOr(&bits[wi], fl ? (uint32_t)(acc >> 32) : 0u);
-        acc = fl ? (acc << 32) : acc;
-        nacc -= fl ? 32u : 0u;
-        wi += fl ? 1u : 0u;
+        const uint32_t s = pp & 31u, w = pp >> 5;
+        const uint64_t v = (uint64_t)val << ((64u - s - n) & 63u);
+        atomicOr(&bits[w], (uint32_t)(v >> 32));
+        atomicOr(&bits[w + 1], (uint32_t)v);
+        pp += n;
       };
       auto put = [&](uint32_t e) { put_n(e >> 5, e & 31u); };   // e == 0: no symbol
       // a pixel's codes composed into one value: 32 bits for every pixel of
@@ -1582,7 +1580,6 @@ __global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
           put_runs(q);
         }
       }
-      if (nacc) atomicOr(&bits[wi], (uint32_t)(acc >> 32));
     }
     __syncthreads();
     // place the tile's bits at its stream offset
