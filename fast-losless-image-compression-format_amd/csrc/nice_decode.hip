@@ -1611,6 +1611,16 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   constexpr unsigned long long* stats = nullptr;
 #endif
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  // per record class: rows back (bits 0-1), pixels back + 3 (bits 2-4), kind
+  // bits (28-31); entries 16.. for row 0.  One LDS read per pixel instead of
+  // three shifts of packed 64-bit constants.
+  __shared__ uint32_t clsw[32];
+  if (threadIdx.x < 32) {
+    const uint32_t c = threadIdx.x & 15u;
+    const unsigned long long kinds = threadIdx.x >= 16 ? ROWS_KIND_Y0 : ROWS_KIND;
+    clsw[threadIdx.x] = ((CLS_ROWS_PACK >> (2 * c)) & 3u) | (uint32_t)((CLS_PX_PACK >> (3 * c)) & 7u) << 2 |
+                        ((uint32_t)(kinds >> (4u * c)) & 15u) << 28;
+  }
   const uint32_t nthr = blockDim.x;
   const uint32_t W = a.W, H = a.H;
   uint32_t* tails = sm;                 // nthr x {lo, len} x 3 (pixels S-1, S-2, S-3)
@@ -1661,15 +1671,16 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   for (uint32_t y = 0; y < H; ++y) {
     const unsigned long long c0 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- pre-pass: records -> per-pixel words
-    const unsigned long long kinds = y == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
+    const uint32_t* const cwt = clsw + (y == 0 ? 16 : 0);
     uint32_t w[S];
 #pragma unroll
     for (int p = 0; p < S; ++p) {
       const uint32_t x = x0 + p;
       const uint32_t r = rec_canon(rn[p], a.rec_tag);
       const uint32_t cls = r >> 24;                          // 0..13
-      const uint32_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
-      const int dx = (int)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;
+      const uint32_t cw = cwt[cls];                          // rows | px + 3 << 2 | kind bits
+      const uint32_t rows = cw & 3u;
+      const int dx = (int)((cw >> 2) & 7u) - 3;
       int tx = (int)x - dx;
       const int wl = tx < 0, wr = tx >= (int)W;
       tx += wl ? (int)W : (wr ? -(int)W : 0);
@@ -1682,7 +1693,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const uint32_t c = spread3(r & 0xFFFFFFu);
       // kind bits from the class (branch-free: the ternary chain compiled to two
       // nested exec-masked branches per pixel)
-      const uint32_t kb = ((uint32_t)(kinds >> (4u * cls)) & 15u) << 28 | (cur ? W_CUR : 0u);
+      const uint32_t kb = (cw & 0xF0000000u) | (cur ? W_CUR : 0u);
       w[p] = kb | ((up && !cur) ? ((o + c) & SP_K) : c) | (cur ? ((uint32_t)tx << 8) : 0u);
     }
     // ---- entry: lane 0 exact (previous row's last pixels; 0 before pixel 0)
