@@ -122,6 +122,32 @@ struct WaveHeap {
     return top;
   }
 
+  // push without the pref-bit upkeep (the initial pushes: no pop walks until
+  // build_prefs has set every bit at once)
+  __device__ void push_plain(unsigned long long x) {
+    const uint32_t e = len++;
+    if (e == 0) { h.key[0] = x; return; }
+    const uint32_t x1 = e + 1u;
+    const uint32_t D = 31u - (uint32_t)__clz((int)x1);
+    const uint32_t ad = (x1 >> (D - min(ln, D))) - 1u;
+    const uint32_t c = (x1 >> (D - min(ln + 1u, D))) - 1u;
+    const unsigned long long old = h.key[ad];
+    const unsigned long long nb = __ballot(ln < D && !gt(old, x));
+    const uint32_t j = nb ? 64u - (uint32_t)__clzll(nb) : 0u;
+    if (ln == j) h.key[ad] = x;
+    if (ln >= j && ln < D) h.key[c] = old;
+  }
+  // every internal node's bit from the heap as it stands (one LDS round)
+  __device__ void build_prefs() {
+    auto pref = [&](uint32_t i) -> uint32_t {   // right child preferred (cnt(right) <= cnt(left))
+      const uint32_t l = 2u * i + 1u, r = l + 1u;
+      const unsigned long long lv = h.key[min(l, 511u)], rv = h.key[min(r, 511u)];
+      return (r < len && !gt(rv, lv)) ? 1u : 0u;
+    };
+    pm = ln < 63u ? pref(ln) : 0u;
+    P = pref(63u + ln) | pref(127u + 2u * ln) << 1 | pref(128u + 2u * ln) << 2;
+  }
+
   __device__ void push(unsigned long long x) {
     const uint32_t e = len++;
     if (e == 0) { h.key[0] = x; return; }
@@ -148,7 +174,8 @@ struct WaveHeap {
 // hfe.rs:63-84 on one wave.  counts[] has n entries.  Writes h.parent.
 __device__ inline void huffman_merge_wave(HeapLds& h, const uint32_t* counts, int n) {
   WaveHeap q(h);
-  for (int i = 0; i < n; ++i) q.push(((unsigned long long)counts[i] << 32) | (unsigned long long)i);
+  for (int i = 0; i < n; ++i) q.push_plain(((unsigned long long)counts[i] << 32) | (unsigned long long)i);
+  q.build_prefs();
   uint32_t next = (uint32_t)n;
   while (q.len > 2) {
     const unsigned long long a = q.pop(), b = q.pop();
