@@ -743,7 +743,10 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
         atomicAdd(&hist[coded && n > 1 ? b2 : dump], 1u);
         atomicAdd(&hist[coded && n > 3 ? b3 : dump], 1u);
       }
-      if (coded) {
+      // a run follows only if the next pixel is uncoded: most coded lanes stop
+      // at this one bit test (lane 63's next pixel is in the next wave: full path)
+      const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
+      if (coded && !next_coded) {
         // next coded pixel: in this wave's 64 pixels from the ballot, else the tile mask
         const unsigned long long above = lane < 63 ? (wbal[q] >> (lane + 1)) : 0ull;
         const int nx = above ? p + 1 + (int)__builtin_ctzll(above) : next_coded_local(mask, p | 63);
