@@ -2,6 +2,9 @@
 // enc_tables (nice_huffman.hpp huffman_merge_wave), lane loops written out,
 // checked against the oracle's literal replay (oracle/nice_oracle.c,
 // hfe.rs:58-87 + std BinaryHeap) on random count vectors with many ties.
+// (The device version skips the pref-bit upkeep during the n initial pushes
+// and sets every bit once before the merge loop; the bits it then holds are
+// the ones this model maintains push by push.)
 // Build: gcc -O2 -c oracle/nice_oracle.c -o /tmp/o.o && g++ -O2 tools/heap_model.cpp /tmp/o.o -Ioracle
 #include <cstdint>
 #include <cstdio>
