@@ -298,6 +298,62 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
                                   "decode": round(n * (N * 4 + sb) / t_dec / 1e9, 2)}}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(gpus, argv):
+    """`--gpus N` with no WORLD_SIZE in the environment: run this script as N
+    ranks under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) in a CHILD process -- no exec, nothing here has touched the GPU
+    -- and return its exit status."""
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(gpus):
+    """World size from torchrun's environment; it must equal --gpus (a bench
+    line's n_gpus is the world size, so a mismatch would mislabel it)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; "
+                         f"launch with --nproc-per-node {gpus} or leave WORLD_SIZE unset")
+    return world
+
+
+def standin(args):
+    """Tests only (`--standin`, CPU, gloo): the launcher, the rank harness and
+    the JSON line of the real bench with a host stand-in step (a fixed amount of
+    byte work per rank), so the N>1 plumbing is exercised without a GPU."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = check_world(args.gpus)
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    buf = np.random.default_rng(rank).integers(0, 256, 1 << 20, dtype=np.uint8)
+    step = (lambda: int(np.bitwise_xor.reduce(buf)))
+    for _ in range(args.warmup):
+        step()
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    el = timed_region(step, args.steps, lambda: None, barrier)
+    el = max_over_ranks(el, dist if world > 1 else None, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "standin", "value": round(world * args.steps * buf.size / el / 1e6, 3),
+                          "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "scaling": "weak"}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -315,10 +371,18 @@ def main():
                          "in 8 bands on one GPU (N=1) (0: skip)")
     ap.add_argument("--check-frames", type=int, default=4,
                     help="frames of the timed batch byte-compared with the oracle (rank 0)")
+    ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.standin:
+        return standin(args)
+
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = check_world(args.gpus)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -495,7 +559,9 @@ def main():
         "cpu_baseline": None,
         "cpu_baseline_threads": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # rank 0 only, after every GPU leg (at N > 1 the other ranks wait at the
+    # final barrier; their GPUs are idle by then)
+    if rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
         try:   # the reference's release profile with target-cpu=native
             flags = O.use_native()
@@ -507,7 +573,9 @@ def main():
         res["cpu_baseline_threads"]["build"] = flags
     if rank == 0:
         print(json.dumps(res))
+        sys.stdout.flush()
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

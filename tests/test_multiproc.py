@@ -49,3 +49,33 @@ def test_two_rank_harness(tmp_path):
     assert job >= 3 * 0.04                                  # rank 1 sleeps 40 ms per step
     s0, s1 = (set(r["seeds"]) for r in sorted(res, key=lambda r: r["rank"]))
     assert not (s0 & s1)                                    # disjoint frame shards
+
+
+def _bench(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", **(env_extra or {}))
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+
+
+def test_bench_gpus_launches_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks itself (child
+    torch.distributed.run) and the line reports the world size."""
+    out = _bench(["--gpus", "2", "--standin", "--steps", "3", "--warmup", "1"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout               # rank 0 only
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["scaling"] == "weak"
+
+
+def test_bench_world_mismatch_fails():
+    out = _bench(["--gpus", "2", "--standin"], {"WORLD_SIZE": "3", "RANK": "0"})
+    assert out.returncode != 0
+    assert "WORLD_SIZE=3" in out.stderr
+
+
+def test_bench_one_rank_standin():
+    out = _bench(["--standin", "--steps", "2", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert json.loads(out.stdout.strip().splitlines()[-1])["n_gpus"] == 1
