@@ -14,6 +14,7 @@
 #include "nice_format.h"
 #include "nice_bits.hpp"
 #include "nice_kernels.h"
+#include "nice_rec.hpp"
 #include "nice_internal.h"
 
 using namespace nice;
@@ -52,17 +53,19 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Encoder scratch layout. The zero-per-launch block comes first (memset once).
 struct EncLayout {
   size_t zero_bytes, total;
-  size_t o_hist, o_flags;
+  size_t o_hist, o_flags, o_ctr, o_status;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_thist, o_gacc;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc;
 };
 
-EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist = true) {
+EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   EncLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
   L.o_hist = take((size_t)n_frames * N_BINS * 4);
   L.o_flags = take((size_t)n_frames * 4 + 4);   // + one word: any frame FLAG_LONG
+  L.o_ctr = take((size_t)n_frames * 4);
+  L.o_status = take((size_t)n_frames * T * 8);
   L.zero_bytes = align_up(o, 16);
   L.o_first = take((size_t)n_frames * T * 4);
   L.o_last = take((size_t)n_frames * T * 4);
@@ -80,7 +83,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx, bool tile_hist
   L.o_tbits = take((size_t)n_frames * T * 4);
   L.o_toff = take((size_t)n_frames * T * 8);
   L.o_dend = take((size_t)n_frames * 8);
-  L.o_thist = take(tile_hist ? (size_t)n_frames * T * TH_WORDS * 4 : 0);
+  L.o_packtab = take((size_t)n_frames * sizeof(PackTab));
   L.o_gacc = take((size_t)n_frames * ((T + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES + 1) * 8);
   L.total = o;
   return L;
@@ -152,6 +155,7 @@ struct nice_ctx {
   uint32_t* rec_region = nullptr;
   uint64_t rec_words = 0, rec_gen = 0;
   uint32_t rec_epoch = 0;
+  int cus = 0;   // compute units of the device (enc_pack's persistent grid)
 };
 
 extern "C" {
@@ -185,6 +189,8 @@ int nice_ctx_create(int device, nice_ctx** out) {
   if (rc) return rc;
   nice_ctx* c = new nice_ctx();
   c->device = device;
+  hipDeviceProp_t prop;
+  c->cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
   *out = c;
   return NICE_OK;
 }
@@ -246,8 +252,16 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.hdr_bitoff = base + L.o_hdrbitoff;
   a.recs = (uint32_t*)(base + L.o_recs);
   a.rec_stride = (N + 3) & ~3ull;
-  a.tile_hist = nullptr;   // set by the ring-classify path
   a.tile_bits = (uint32_t*)(base + L.o_tbits);
+  a.packtab = base + L.o_packtab;
+  a.pack_ctr = (uint32_t*)(base + L.o_ctr);
+  {   // frames packed at once: <= 64, dividing the frames about evenly
+    const uint32_t per = (n_frames + 63) / 64;
+    a.pack_slots = (n_frames + per - 1) / per;
+  }
+  a.status = (unsigned long long*)(base + L.o_status);
+  a.pack_mode = 0;
+  a.long_only = 1;
   a.tile_off = (unsigned long long*)(base + L.o_toff);
   a.data_end = (unsigned long long*)(base + L.o_dend);
   a.tile_lo = 0;
@@ -280,8 +294,10 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   const uint32_t T = tiles_for(w, h);
-  const bool ring = channels == 4 && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
-  EncLayout L = enc_layout(n_frames, T, N, ring);
+  const bool aligned = ((uintptr_t)d_px & 3) == 0 && (frame_stride & 3) == 0;
+  const bool ring = aligned && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
+  if ((uint64_t)n_frames * T >= (1ull << 32)) return NICE_E_ARG;   // enc_pack's 32-bit work counter
+  EncLayout L = enc_layout(n_frames, T, N);
   int rc = ctx->enc.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->enc.ptr;
@@ -306,8 +322,10 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     a.tiles_per_block = (uint32_t)per;
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
-    if (ring) a.tile_hist = (uint32_t*)(base + L.o_thist);
-    if (ring) hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    if (ring && channels == 4)
+      hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    else if (ring)
+      hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
     else if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     tm.end(st);
@@ -323,24 +341,26 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   hipLaunchKernelGGL(enc_header, dim3(n_frames), dim3(64), 0, st, a);
   ctx->timer.end(st);
   if (T > 0) {
-    // grid-stride over tiles: 8 blocks of 256 threads per CU (LDS ~21 KB each)
-    const uint32_t tblocks = (uint32_t)(total_tiles < 2048 ? total_tiles : 2048);
     ctx->timer.begin(NICE_PH_ENC_TILEBITS, st);
-    if (a.tile_hist) hipLaunchKernelGGL(enc_tilebits_hist, dim3(tblocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_packtab, dim3(n_frames), dim3(256), 0, st, a);
     ctx->timer.end(st);
-    ctx->timer.begin(NICE_PH_ENC_TILESCAN, st);
+    // frames with codes over 25 bits or composed entries over 32 (FLAG_LONG;
+    // the launches return at once for the others): tile bits, their scan,
+    // codes that fit the cache, then the wrapped writes
+    const uint32_t tblocks = (uint32_t)(total_tiles < 2048 ? total_tiles : 2048);
+    ctx->timer.begin(NICE_PH_ENC_LONG, st);
+    hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
     if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, n_frames), dim3(256), 0, st, a, 1);
     hipLaunchKernelGGL(enc_tilescan, dim3(a.groups, n_frames), dim3(1024), 0, st, a);
-    ctx->timer.end(st);
-    ctx->timer.begin(NICE_PH_ENC_PACK, st);
-    hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
-    ctx->timer.end(st);
-    // frames with codes over 25 bits (FLAG_LONG; the launches return at once
-    // for the others): codes that fit the cache, then the wrapped writes
-    ctx->timer.begin(NICE_PH_ENC_LONG, st);
     hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
     hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);
+    ctx->timer.end(st);
+    // every other frame: one pass, tile offsets by look-back
+    const uint64_t pblocks = std::min<uint64_t>(total_tiles, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU);
+    ctx->timer.begin(NICE_PH_ENC_PACK, st);
+    hipLaunchKernelGGL(enc_pack, dim3((uint32_t)pblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_edges, dim3(std::min<uint32_t>((T + 255) / 256, 64u), std::min<uint32_t>(n_frames, 4096u)),
+                       dim3(256), 0, st, a);
     ctx->timer.end(st);
     ctx->timer.begin(NICE_PH_ENC_TAIL, st);
     hipLaunchKernelGGL(enc_tail, dim3((n_frames + 63) / 64), dim3(64), 0, st, a);
@@ -723,7 +743,7 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (channels == 4 && ((uintptr_t)d_px & 3)) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
-  EncLayout L = enc_layout(1, T, band_px1 - band_px0, false);
+  EncLayout L = enc_layout(1, T, band_px1 - band_px0);
   int rc = ctx->band.grow(L.total);
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->band.ptr;
@@ -739,6 +759,8 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   a.px_lo = (int64_t)px0;
   a.px_hi = (int64_t)(px0 + px_count);
   a.band = 1;
+  a.pack_mode = 1;   // tile offsets from enc_tilescan (the band's bit offset comes from the exchange)
+  a.long_only = 0;
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
   const uint64_t work = tile_hi - tile_lo;
   uint64_t blocks = 2048, per = (work + blocks - 1) / blocks;
@@ -783,6 +805,7 @@ int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, 
   h.out_stride = 4096;
   h.out_len = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
   hipLaunchKernelGGL(enc_header, dim3(1), dim3(64), 0, st, h);
+  hipLaunchKernelGGL(enc_packtab, dim3(1), dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_tilebits, dim3(std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u)), dim3(256), 0, st, a);
   unsigned long long* info = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
   hipLaunchKernelGGL(enc_band_sum, dim3(1), dim3(256), 0, st, a, info);
@@ -817,7 +840,9 @@ int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_
   const uint32_t tblocks = std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u);
   if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, 1), dim3(256), 0, st, a, 1);
   hipLaunchKernelGGL(enc_tilescan, dim3(a.groups, 1), dim3(1024), 0, st, a);
-  hipLaunchKernelGGL(enc_pack, dim3(tblocks), dim3(256), 0, st, a);
+  NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
+  hipLaunchKernelGGL(enc_pack, dim3((uint32_t)std::min<uint64_t>(a.tile_hi - a.tile_lo, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU)),
+                     dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);
   NICE_HIP(hipGetLastError());

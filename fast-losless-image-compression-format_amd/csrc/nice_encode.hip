@@ -29,6 +29,7 @@
 #include "nice_format.h"
 #include "nice_huffman.hpp"
 #include "nice_kernels.h"
+#include "nice_rec.hpp"
 
 namespace nice {
 
@@ -216,6 +217,21 @@ __device__ __forceinline__ uint32_t rec_bins(const RecBinTable& t, uint32_t rec,
   b2 = (ra.z >> 16) + __builtin_amdgcn_ubfe(rec, ra.z, rb.z);
   b3 = (ra.w >> 16) + __builtin_amdgcn_ubfe(rec, ra.w, rb.w);
   return rb.x >> 8;
+}
+
+// Window-classify record (layout above) -> the packer's record (nice_rec.hpp).
+__device__ __forceinline__ uint32_t rec2_from_old(uint32_t rec, uint32_t lane) {
+  const uint32_t m = rec & 7u;
+  if (m == REC_UNCODED) return rec2_unc(lane);
+  if (m == P_BACK_REF) return ((C0_BR + ((rec >> 3) & 7u)) << 3) | rec2_abs(lane);
+  if (m == P_SMALL_DIFF) return ((C0_SD + ((rec >> 3) & 0x1FFu)) << 3) | rec2_abs(lane);
+  if (m == P_LUMA2)
+    return ((C0_L2 + ((rec >> 13) & 0x3Fu)) << 3) | ((SX_L2 + ((rec >> 3) & 0x1Fu)) << 14) |
+           ((SX_L2 + ((rec >> 23) & 0x1Fu)) << 23);
+  if (m == P_LUMA)
+    return ((C0_LUMA + 64u * ((rec >> 3) & 15u) + ((rec >> 17) & 0x3Fu)) << 3) |
+           ((SX_LUMA + ((rec >> 7) & 0x1Fu)) << 14) | ((SX_LUMA + ((rec >> 27) & 0x1Fu)) << 23);
+  return (((rec >> 3) & 0xFFu) << 3) | (((rec >> 13) & 0xFFu) << 14) | (((rec >> 23) & 0xFFu) << 23);
 }
 
 // Each mode's identifying stream and symbols per pixel (code.rs:191-366):
@@ -406,7 +422,7 @@ __device__ __forceinline__ void enc_classify_body(const EncArgs& a) {
         const uint32_t rf = classify_fast<true>(tw, p + 3, (uint32_t)(start + p), a.W);
         rec = coded ? rf : REC_UNCODED;
       }
-      if (p < count) recs[p] = rec;
+      if (p < count) recs[p] = rec2_from_old(rec, (uint32_t)lane);
       if (coded) {
         uint32_t b0, b1, b2, b3;
         const uint32_t n = rec_bins(rec, b0, b1, b2, b3);
@@ -500,7 +516,7 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 // i-1 can never hit a coded pixel, so it is not tested.)
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
-                                                  uint32_t i, const uint32_t* ltab) {
+                                                  uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
   const uint32_t* b0 = ring + ((s - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b1 = ring + ((s - W - 3u) & (CLS_RING - 1)) + tid;
   const uint32_t* b2 = ring + ((s - 2u * W) & (CLS_RING - 1)) + tid;
@@ -565,22 +581,58 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
     }
   }
   const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
-  const uint32_t rec_br = P_BACK_REF | (bk << 3);
-  const uint32_t rec_sd = P_SMALL_DIFF | (sdi << 3);
-  // LUMA2 and LUMA keep the luma-space fields in place (LUMA: after its 4-bit reference)
-  const uint32_t lf = (l2 ? t2 : lt) & LUMA_FIELDS;
-  const uint32_t rec_l2 = P_LUMA2 | (lf << 3);
-  const uint32_t rec_lu = P_LUMA | (lk << 3) | (lf << 7);
-  const uint32_t rec_rgb = P_RGB | ((r & K3(0xFFu)) << 3);
-  return br ? rec_br : sd ? rec_sd : l2 ? rec_l2 : lk < 11u ? rec_lu : rec_rgb;
+  // the record (nice_rec.hpp): BACK_REF and SMALL_DIFF onto the lane's
+  // constant (mode range + absent slots); RGB's r, g, b fields (spread, 10-bit
+  // spacing) to c0, s1, s2 by doubling g (one bit further up); LUMA2 / LUMA: g
+  // (luma-space field 1) to c0 with the mode range (LUMA: + 64 k), r and b to
+  // s1 and s2
+  const uint32_t rec_br = (bk << 3) + cbr;
+  const uint32_t rec_sd = (sdi << 3) + csd;
+  const uint32_t rs = r & K3(0xFFu);
+  const uint32_t rec_rgb = (rs + (rs & (0xFFu << 10))) << 3;
+  const uint32_t lf = l2 ? t2 : lt;
+  const uint32_t lbase = l2 ? ((C0_L2 << 3) | (SX_L2 << 14) | (SX_L2 << 23))
+                            : ((C0_LUMA << 3) | (SX_LUMA << 14) | (SX_LUMA << 23)) + (lk << 9);
+  const uint32_t rec_lu = lbase + (__builtin_amdgcn_ubfe(lf, 10, 6) << 3) + ((lf & 0x1Fu) << 14) +
+                          ((lf & (0x1Fu << 20)) << 3);
+  return br ? rec_br : sd ? rec_sd : (l2 || lk < 11u) ? rec_lu : rec_rgb;
 }
 
-__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
+// slot histogram (nice_rec.hpp) add of one record: three unconditional LDS
+// adds (run members and absent slots land on the lane's own zero slots)
+__device__ __forceinline__ void slot_hist_add(uint32_t* hs, uint32_t rec) {
+  char* hb = reinterpret_cast<char*>(hs);
+  atomicAdd(reinterpret_cast<uint32_t*>(hb + ((rec >> 1) & 0x1FFCu)), 1u);
+  atomicAdd(reinterpret_cast<uint32_t*>(hb + C0_N * 4 + ((rec >> 12) & 0x7FCu)), 1u);
+  atomicAdd(reinterpret_cast<uint32_t*>(hb + (C0_N + SX_N) * 4 + ((rec >> 21) & 0x7FCu)), 1u);
+}
+
+// RGB frames (C = 3, 4-byte aligned frames): a tile's 3072 bytes arrive as 768
+// dwords (one or two per thread), are staged in LDS and each pixel's 3 bytes
+// are taken with one funnel shift of two dwords.
+constexpr int RGB_TILE_DW = ENC_TILE * 3 / 4;   // 768
+__device__ __forceinline__ uint32_t rgb_dword(const uint8_t* fr, uint64_t nbytes, uint64_t j) {
+  if (4 * j + 4 <= nbytes) return reinterpret_cast<const uint32_t*>(fr)[j];
+  uint32_t v = 0;
+  for (int k = 0; k < 4; ++k)
+    if (4 * j + k < nbytes) v |= (uint32_t)fr[4 * j + k] << (8 * k);
+  return v;
+}
+// pixel j of a frame as R | G << 8 | B << 16 (what y_from_rgba reads)
+template <int C>
+__device__ __forceinline__ uint32_t px_word(const uint8_t* fr, int64_t j) {
+  if (C == 4) return reinterpret_cast<const uint32_t*>(fr)[j];
+  const uint8_t* p = fr + 3 * j;
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+}
+
+template <int C>
+__device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
   __shared__ uint32_t ring[CLS_RING + CLS_GUARD];
-  __shared__ uint32_t hist[N_BINS + 64];   // + a discard slot per lane (absent symbols)
-  __shared__ uint32_t snap[N_BINS];        // hist after the previous tile
+  __shared__ uint32_t stage[C == 3 ? RGB_TILE_DW + 4 : 1];
+  __shared__ uint32_t hs[C0_N + 2 * SX_N];     // slot histogram (nice_rec.hpp)
+  __shared__ uint32_t run_hist[8];             // run digits (prefixes 5..12)
   __shared__ uint32_t mask[ENC_TILE / 32];
-  __shared__ RecBinTable rbt;
   __shared__ uint32_t ltab[2][CLS_PPT][16];   // [tile parity][q][luma reference]: ring index for thread 0
   const uint32_t T = a.tiles_per_frame;
   const uint64_t total_work = (uint64_t)a.n_frames * T;
@@ -588,29 +640,38 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
   if (w_begin >= w_end) return;
   const int tid = threadIdx.x, lane = tid & 63;
-  rbt_init(rbt, tid);
+  // the lane's record constants: BACK_REF / SMALL_DIFF ranges with absent
+  // slots, and the run-member record
+  const uint32_t cbr = (C0_BR << 3) | rec2_abs((uint32_t)lane), csd = (C0_SD << 3) | rec2_abs((uint32_t)lane);
+  const uint32_t cunc = rec2_unc((uint32_t)lane);
   // back distance of luma reference k (code.rs:293-339), for the tile tables
   const uint32_t lback = tid < 16 * CLS_PPT && (tid & 15) < 11
                              ? (uint32_t)lr_rows(tid & 15) * a.W + (uint32_t)lr_px(tid & 15) : 0u;
   const uint32_t W = a.W;
   const int64_t N = (int64_t)W * a.H;
-  for (int b = tid; b < N_BINS; b += CLS_THREADS) { hist[b] = 0; snap[b] = 0; }
+  for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+  if (tid < 8) run_hist[tid] = 0;
+  // the frame's symbol counts into the 858 bins (hfe.rs:29-45), once per
+  // block and frame
   auto flush = [&](uint32_t frame) {
     __syncthreads();
     for (int b = tid; b < N_BINS; b += CLS_THREADS) {
-      if (hist[b]) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], hist[b]);
-      hist[b] = 0;
-      snap[b] = 0;
+      uint32_t v = slot_hist_bin(hs, b);
+      if (b >= BIN_PREFIX + P_RUN1 && b < BIN_PREFIX + P_RUN1 + 8) v += run_hist[b - BIN_PREFIX - P_RUN1];
+      if (v) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], v);
     }
+    __syncthreads();
+    for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+    if (tid < 8) run_hist[tid] = 0;
   };
   // prefill: the 3 rows + 3 pixels before the first tile
   uint32_t cur_frame = (uint32_t)(w_begin / T);
   {
     const int64_t start = (int64_t)(w_begin % T) * ENC_TILE;
     const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
-    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)cur_frame * a.frame_stride);
+    const uint8_t* fr = a.px + (uint64_t)cur_frame * a.frame_stride;
     for (int64_t j = lo + tid; j < start; j += CLS_THREADS) {
-      const uint32_t k = (uint32_t)j & (CLS_RING - 1), y = y_from_rgba(fr[j]);
+      const uint32_t k = (uint32_t)j & (CLS_RING - 1), y = y_from_rgba(px_word<C>(fr, j));
       ring[k] = y;
       if (k < CLS_GUARD) ring[CLS_RING + k] = y;
     }
@@ -620,31 +681,20 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
   auto fetch = [&](const TileIter& ti, uint32_t (&v)[CLS_PPT]) {
     const uint32_t f = ti.f;
     const int64_t start = (int64_t)ti.tt() * ENC_TILE;
-    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
+    if (C == 4) {
+      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
 #pragma unroll
-    for (int q = 0; q < CLS_PPT; ++q) {
-      const int64_t j = start + q * CLS_THREADS + tid;
-      v[q] = j < N ? fr[j] : 0u;
-    }
-  };
-  // this tile's symbol counts (histogram growth since the previous tile), for
-  // enc_tilebits_hist: 858 u16 counts as u32 pairs.  Taken for tile t after
-  // the staging barrier of tile t + 1 (every atomic of t is done, none of t + 1
-  // has started): no barrier of its own.
-  uint64_t prev_t = ~0ull;
-  auto snap_tile = [&]() {
-    if (prev_t != ~0ull && tid < (int)TH_WORDS) {
-      uint32_t wv = 0;
-      if (2 * tid < N_BINS) {
-        const int b = 2 * tid;
-        const uint32_t h0 = hist[b], h1 = hist[b + 1];
-        wv = ((h0 - snap[b]) & 0xFFFFu) | ((h1 - snap[b + 1]) << 16);
-        snap[b] = h0;
-        snap[b + 1] = h1;
+      for (int q = 0; q < CLS_PPT; ++q) {
+        const int64_t j = start + q * CLS_THREADS + tid;
+        v[q] = j < N ? fr[j] : 0u;
       }
-      a.tile_hist[prev_t * TH_WORDS + tid] = wv;
+    } else {   // the tile's dwords tid and 512 + tid
+      const uint8_t* fr = a.px + (uint64_t)f * a.frame_stride;
+      const uint64_t j0 = (uint64_t)ti.tt() * RGB_TILE_DW, nbytes = (uint64_t)N * 3;
+      v[0] = 4 * (j0 + tid) < nbytes ? rgb_dword(fr, nbytes, j0 + tid) : 0u;
+      v[1] = tid < RGB_TILE_DW - CLS_THREADS && 4 * (j0 + CLS_THREADS + tid) < nbytes
+                 ? rgb_dword(fr, nbytes, j0 + CLS_THREADS + tid) : 0u;
     }
-    prev_t = ~0ull;
   };
   TileIter it(a, w_begin), nx(a, w_begin);
   fetch(nx, pf);
@@ -652,17 +702,29 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     const uint32_t f = it.f;
     const uint32_t tt = it.tt();
     if (f != cur_frame) {
-      __syncthreads();
-      snap_tile();
       flush(cur_frame);
       cur_frame = f;
     }
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)min((int64_t)ENC_TILE, N - start);
     // stage this tile (Y space), start loading the next
+    uint32_t pxw[CLS_PPT];
+    if (C == 4) {
+#pragma unroll
+      for (int q = 0; q < CLS_PPT; ++q) pxw[q] = pf[q];
+    } else {   // bytes via LDS: the previous tile's readers are past its staging barrier
+      stage[tid] = pf[0];
+      if (tid < RGB_TILE_DW - CLS_THREADS) stage[CLS_THREADS + tid] = pf[1];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < CLS_PPT; ++q) {
+        const uint32_t b = 3u * (uint32_t)(q * CLS_THREADS + tid);
+        pxw[q] = __builtin_amdgcn_alignbit(stage[(b >> 2) + 1], stage[b >> 2], (b & 3u) * 8u);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
-      const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (CLS_RING - 1), y = y_from_rgba(pf[q]);
+      const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (CLS_RING - 1), y = y_from_rgba(pxw[q]);
       ring[k] = y;
       if (k < CLS_GUARD) ring[CLS_RING + k] = y;
     }
@@ -674,7 +736,6 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
     nx.step(1);
     if (w + 1 < w_end) fetch(nx, pf);
     __syncthreads();
-    snap_tile();
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
     unsigned long long wbal[CLS_PPT];   // coded flags of the wave's 64 pixels per q
@@ -718,31 +779,20 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
       const bool coded = (coded_bits >> q) & 1u;
       uint32_t rf;
       if (fast)   // block-uniform: both variants are straight-line code
-        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q]);
+        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q],
+                                  cbr, csd);
       else
         rf = classify_ring<true>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p),
-                                 nullptr);
-      rec[q] = coded ? rf : REC_UNCODED;
+                                 nullptr, cbr, csd);
+      rec[q] = coded ? rf : cunc;
     }
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
       const int p = q * CLS_THREADS + tid;
       const bool coded = (coded_bits >> q) & 1u;
       if (p < count) recs[p] = rec[q];
-      // the mode prefixes (bins BIN_PREFIX + 0..4) are not counted here: each
-      // mode emits a fixed number of symbols into one stream of its own, so
-      // enc_tables and enc_tilebits_hist derive them (mode_prefix_count)
-      {
-        // payload symbols: four unconditional LDS adds, absent ones into this
-        // lane's discard slot (no divergent branches)
-        uint32_t b0, b1, b2, b3;
-        const uint32_t n = rec_bins(rbt, rec[q], b0, b1, b2, b3);
-        const uint32_t dump = N_BINS + (uint32_t)lane;
-        atomicAdd(&hist[coded ? b0 : dump], 1u);
-        atomicAdd(&hist[coded && n > 1 ? b1 : dump], 1u);
-        atomicAdd(&hist[coded && n > 1 ? b2 : dump], 1u);
-        atomicAdd(&hist[coded && n > 3 ? b3 : dump], 1u);
-      }
+      // payload symbols (the mode prefixes are derived from them by enc_tables)
+      slot_hist_add(hs, rec[q]);
       // a run follows only if the next pixel is uncoded: most coded lanes stop
       // at this one bit test (lane 63's next pixel is in the next wave: full path)
       const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
@@ -753,19 +803,18 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
         if (nx < count && nx > p + 1) {
           uint64_t mm = (uint64_t)(nx - p - 2);
           while (true) {
-            atomicAdd(&hist[BIN_PREFIX + P_RUN1 + (uint32_t)(mm & 7u)], 1u);
+            atomicAdd(&run_hist[(uint32_t)(mm & 7u)], 1u);
             if (mm < 8) break;
             mm >>= 3;
           }
         }
       }
     }
-    prev_t = (uint64_t)f * T + tt;
   }
-  __syncthreads();
-  snap_tile();
   flush(cur_frame);
 }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3>(a); }
 
 // ---------------------------------------------------------------------------
 // K2: runs crossing tile ends. One block (1024 threads) per frame.
@@ -775,6 +824,7 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) {
 __global__ __launch_bounds__(256) void enc_group_reduce(EncArgs a, int what) {
   __shared__ unsigned long long part[4];
   const uint32_t g = blockIdx.x, f = blockIdx.y;
+  if (what == 1 && a.long_only && !(a.frame_flags[f] & FLAG_LONG)) return;   // bit totals: long path only
   const uint32_t nt = a.tile_hi - a.tile_lo;
   const uint32_t t0 = g * ENC_GROUP_TILES, t1 = min(t0 + ENC_GROUP_TILES, nt);
   const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo;
@@ -1182,31 +1232,37 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K5-K7: bit placement without a serial dependency.
-//   enc_tilebits  per tile: bits of its pixels (prefix, payload, run digits)
-//   enc_tilescan  per frame: exclusive scan of tile bits from the data start;
-//                 zeroes every output word two tiles (or a tile and the tail)
-//                 share, so enc_pack can OR those and store the rest
-//   enc_pack      per tile: codes MSB-first into an LDS bit buffer, then
-//                 shifted to the tile's offset: interior words stored, the
-//                 first/last partial words OR-ed (bitwriter.rs:55-73)
+// K5-K7: bit placement.
+//   enc_packtab   per frame: the packer's code tables (nice_rec.hpp PackTab):
+//                 each record slot -> {code, length}, T0 with the mode prefix
+//                 composed in front, run digits composed per run length;
+//                 FLAG_LONG for frames an entry of which exceeds 32 bits
+//   enc_pack      per tile, one pass: the pixels' codes from three lookups
+//                 each, a block scan of their lengths, the tile's stream
+//                 offset by a decoupled look-back over the preceding tiles'
+//                 status words (pack_mode 0; bands: from enc_tilescan,
+//                 pack_mode 1), codes MSB-first into an LDS bit buffer
+//                 (bitwriter.rs:55-73), then shifted to the offset and stored
+//   enc_edges     ORs each tile's first partial word into the word the tile
+//                 before it (or the header) wrote
 //   enc_tail      per frame: [P, P, 0, 0, 0] after the data (hfe.rs:115,
 //                 code.rs:421-422) and the stream length
+// FLAG_LONG frames (a code over FAST_MAX_CODE_BITS, or a composed entry over
+// 32 bits) take enc_tilebits -> enc_tilescan -> enc_pack_long instead.
 // A thread owns 4 consecutive pixels and reads their records with one 16-byte
 // load.
 // ---------------------------------------------------------------------------
-constexpr int PACK_MAX_WORDS = ENC_TILE * 128 / 32 + 2;   // <= 125 bits/px with 25-bit codes
+constexpr int PACK_SUB = 4;                                // tiles per enc_pack work item
+constexpr int PACK_CAP_BITS = PACK_SUB * ENC_TILE * 32;    // LDS bit buffer: <= 32 bits per pixel
+constexpr int PACK_MAX_WORDS = PACK_CAP_BITS / 32 + 2;
+constexpr int PK_THREADS = 256;
 
 struct TileQuad {
   uint32_t rc[4];
   uint32_t nib;        // coded flags of the 4 pixels
-  uint64_t run[4];     // run after each coded pixel
-  uint32_t nb;         // bits of the 4 pixels
-  uint32_t e[4][5];    // code table entries: prefix + up to 4 payload symbols (0: none)
 };
 
-// The thread's 4 records of tile t (REC_UNCODED past the frame end); issued one
-// tile ahead so the loads overlap the previous tile's work.
+// The thread's 4 records of tile tt of frame f (run members past the frame end).
 __device__ __forceinline__ void quad_fetch(const EncArgs& a, uint32_t f, uint32_t tt, int p0, uint32_t (&rc)[4]) {
   const int64_t N = (int64_t)a.W * a.H;
   const int64_t start = (int64_t)tt * ENC_TILE;
@@ -1217,87 +1273,58 @@ __device__ __forceinline__ void quad_fetch(const EncArgs& a, uint32_t f, uint32_
     rc[0] = v.x; rc[1] = v.y; rc[2] = v.z; rc[3] = v.w;
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rc[q] = (p0 + q < count) ? rp[q] : REC_UNCODED;
+    for (int q = 0; q < 4; ++q) rc[q] = (p0 + q < count) ? rp[q] : rec2_unc(0);
   }
 }
 
-// Builds the tile's coded mask from the records (LDS, needs a barrier before
-// use) -- phase 1.
+// The tile's coded mask from the records (LDS, needs a barrier before use).
 __device__ __forceinline__ void quad_mask(const uint32_t (&rc)[4], int lane, int wid, uint32_t* mask,
                                           TileQuad& Q) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) Q.rc[q] = rc[q];
   Q.nib = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) Q.nib |= ((Q.rc[q] & 7u) != REC_UNCODED ? 1u : 0u) << q;
+  for (int q = 0; q < 4; ++q) Q.nib |= (rec2_coded(Q.rc[q]) ? 1u : 0u) << q;
   const uint32_t mw = wave_or8(Q.nib << (4 * (lane & 7)));
   if ((lane & 7) == 0) mask[wid * 8 + (lane >> 3)] = mw;
 }
 
-// Runs, code entries and bit counts -- phase 2 (after the mask barrier).
-// Branch-free apart from the run digits: absent symbols get entry 0 (length 0).
-__device__ __forceinline__ void quad_bits(const uint32_t* tbl, const RecBinTable& rbt, const uint32_t* mask,
-                                          int64_t start, int count, int p0, uint32_t next_tile_px, TileQuad& Q) {
+// Run after each of the thread's 4 pixels (0 for run members): the next coded
+// pixel in the thread's quad, else in the tile (mask), else tile_next.  Pixel
+// indices are < 2^30 (the boundary's frame cap): 32-bit arithmetic.
+__device__ __forceinline__ void quad_runs(const uint32_t* mask, int64_t start, int count, int p0,
+                                          uint32_t next_tile_px, const TileQuad& Q, uint32_t (&run)[4]) {
   const int nx_local = next_coded_local(mask, p0 + 3);
-  const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)next_tile_px;
-  Q.nb = 0;
+  const uint32_t s32 = (uint32_t)start + (uint32_t)p0;
+  const uint32_t after = (nx_local < count) ? (uint32_t)start + (uint32_t)nx_local : next_tile_px;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const bool coded = (Q.nib >> q) & 1u;
-    uint32_t b0, b1, b2, b3;
-    const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
-    const uint32_t t0 = tbl[BIN_PREFIX + min(Q.rc[q] & 7u, 4u)], t1 = tbl[b0], t2 = tbl[b1], t3 = tbl[b2],
-                   t4 = tbl[b3];
-    Q.e[q][0] = coded ? t0 : 0u;
-    Q.e[q][1] = coded ? t1 : 0u;
-    Q.e[q][2] = (coded && n > 1) ? t2 : 0u;
-    Q.e[q][3] = (coded && n > 1) ? t3 : 0u;
-    Q.e[q][4] = (coded && n > 3) ? t4 : 0u;
-    Q.nb += (Q.e[q][0] & 31u) + (Q.e[q][1] & 31u) + (Q.e[q][2] & 31u) + (Q.e[q][3] & 31u) + (Q.e[q][4] & 31u);
     const uint32_t later = Q.nib >> (q + 1);
-    const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
-    Q.run[q] = coded ? nxt - (uint64_t)(start + p0 + q) - 1 : 0u;
-    if (Q.run[q] > 0) {
-      uint64_t m = Q.run[q] - 1;
-      while (true) {
-        Q.nb += tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)] & 31u;
-        if (m < 8) break;
-        m >>= 3;
-      }
-    }
+    const uint32_t nxt = later ? s32 + (uint32_t)(q + 1) + (uint32_t)__builtin_ctz(later) : after;
+    run[q] = ((Q.nib >> q) & 1u) ? nxt - (s32 + (uint32_t)q) - 1u : 0u;
   }
 }
 
-__device__ __forceinline__ void load_tbl(uint32_t* tbl, const EncArgs& a, uint32_t f) {
-  for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) tbl[b] = a.tbl[(uint64_t)f * N_BINS + b];
-}
 __device__ __forceinline__ void load_lens(uint32_t* lens, const EncArgs& a, uint32_t f) {
   for (int b = threadIdx.x; b < N_BINS; b += ENC_THREADS) lens[b] = a.tbl_len8[(uint64_t)f * N_BINS + b];
 }
 
 // Bits of the thread's 4 pixels (prefix, payload, run digits) from full code
-// lengths (any length: also the frames with codes over FAST_MAX_CODE_BITS).
-__device__ __forceinline__ uint32_t quad_nbits(const uint32_t* lens, const RecBinTable& rbt, const uint32_t* mask,
-                                               int64_t start, int count, int p0, uint32_t next_tile_px,
-                                               const TileQuad& Q) {
-  const int nx_local = next_coded_local(mask, p0 + 3);
-  const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)next_tile_px;
+// lengths (any length).
+__device__ __forceinline__ uint32_t quad_nbits(const uint32_t* lens, const uint32_t* mask, int64_t start, int count,
+                                               int p0, uint32_t next_tile_px, const TileQuad& Q) {
+  uint32_t run[4];
+  quad_runs(mask, start, count, p0, next_tile_px, Q, run);
   uint32_t nb = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    if (!((Q.nib >> q) & 1u)) continue;
-    uint32_t b0, b1, b2, b3;
-    const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
-    nb += lens[BIN_PREFIX + min(Q.rc[q] & 7u, 4u)] + lens[b0];
-    if (n > 1) nb += lens[b1] + lens[b2];
-    if (n > 3) nb += lens[b3];
-    const uint32_t later = Q.nib >> (q + 1);
-    const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
-    const uint64_t run = nxt - (uint64_t)(start + p0 + q) - 1;
-    if (run > 0) {
-      uint64_t m = run - 1;
+    uint32_t b[5];
+    const uint32_t n = rec2_syms(Q.rc[q], b);
+    for (uint32_t k = 0; k < n; ++k) nb += lens[b[k]];
+    if (run[q] > 0) {
+      uint32_t m = run[q] - 1;
       while (true) {
-        nb += lens[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
+        nb += lens[BIN_PREFIX + P_RUN1 + (m & 7u)];
         if (m < 8) break;
         m >>= 3;
       }
@@ -1307,8 +1334,7 @@ __device__ __forceinline__ uint32_t quad_nbits(const uint32_t* lens, const RecBi
 }
 
 // Contiguous tile ranges per block (the code table is reloaded only when the
-// frame changes); records are fetched one tile ahead.
-// Work items w in [w0, w1): frame w / nt, band tile tile_lo + w % nt.
+// frame changes).  Work items w in [w0, w1): frame w / nt, band tile tile_lo + w % nt.
 __device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& w0, uint64_t& w1) {
   const uint64_t total = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
   const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
@@ -1316,27 +1342,29 @@ __device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& w0, uint6
   w1 = w0 + per < total ? w0 + per : total;
 }
 
+// frames the long-code path handles: all (bands), or those with FLAG_LONG
+__device__ __forceinline__ bool long_path(const EncArgs& a, uint32_t f) {
+  return !a.long_only || (a.frame_flags[f] & FLAG_LONG);
+}
+
 __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
   __shared__ uint32_t tbl[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
-  __shared__ RecBinTable rbt;
-  rbt_init(rbt, threadIdx.x);
+  if (a.long_only && !(a.frame_flags[a.n_frames] & FLAG_LONG)) return;   // no long-code frame in the batch
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t N = (int64_t)a.W * a.H;
   const int p0 = 4 * threadIdx.x;
   uint32_t cur_f = 0xFFFFFFFFu;
   uint64_t t0, t1;
   tile_range(a, t0, t1);
-  uint32_t rn[4];
-  TileIter it(a, t0), nx(a, t0);
-  if (t0 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
+  TileIter it(a, t0);
   for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
     const uint64_t t = it.tile();
-    uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    nx.step(1);
-    if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
     const uint32_t f = it.f, tt = it.tt();
+    if (!long_path(a, f)) continue;   // block-uniform
+    uint32_t rc[4];
+    quad_fetch(a, f, tt, p0, rc);
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
     __syncthreads();
@@ -1344,82 +1372,12 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
     TileQuad Q;
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
-    uint32_t x = quad_nbits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
+    uint32_t x = quad_nbits(tbl, mask, start, count, p0, a.tile_next[t], Q);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
     if (lane == 0) wsum[wid] = x;
     __syncthreads();
     if (threadIdx.x == 0) a.tile_bits[t] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  }
-}
-
-// Tile bits from the per-tile symbol counts of enc_classify_ring: sum of
-// count x code length over the 858 bins, plus the run digits of the tile's
-// last run (it ends at tile_next, in a later tile; code.rs:371-407).  One wave
-// per tile, no block barriers: each wave keeps the code lengths of its current
-// frame in its own LDS slice.
-__global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
-  __shared__ uint32_t lens_all[4][2 * TH_WORDS];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t* lens = lens_all[wid];
-  uint32_t cur_f = 0xFFFFFFFFu, prefix_len_rgb = 0;
-  uint64_t t0, t1;
-  tile_range(a, t0, t1);
-  TileIter it(a, t0 + wid);
-  for (uint64_t w = t0 + wid; w < t1; w += 4, it.step(4)) {
-    const uint64_t t = it.tile();
-    const uint32_t f = it.f;
-    if (f != cur_f) {
-      __builtin_amdgcn_wave_barrier();
-      // the mode prefixes are not in the tile counts: each mode's prefix length
-      // rides on the bins of its identifying stream (RGB: once per 3 symbols)
-      const uint8_t* l8 = a.tbl_len8 + (uint64_t)f * N_BINS;
-      uint32_t pl[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) pl[k] = l8[BIN_PREFIX + k];
-      prefix_len_rgb = pl[P_RGB];
-      for (int b = lane; b < (int)(2 * TH_WORDS); b += 64) {
-        uint32_t v = b < N_BINS ? (uint32_t)l8[b] : 0u;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) v += (k != P_RGB && mode_id_bin(k, b)) ? pl[k] : 0u;
-        lens[b] = v;
-      }
-      cur_f = f;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    }
-    const uint32_t* th = a.tile_hist + t * TH_WORDS;
-    uint32_t acc = 0, rgb = 0;
-#pragma unroll
-    for (int k0 = 0; k0 < (int)TH_WORDS; k0 += 64) {
-      const int k = k0 + lane;
-      if (k < (int)TH_WORDS) {
-        const uint32_t v = th[k];
-        acc += (v & 0xFFFFu) * lens[2 * k] + (v >> 16) * lens[2 * k + 1];
-        if (2 * k < 256) rgb += (v & 0xFFFFu) + (v >> 16);   // SC_RGB symbols: 3 per RGB pixel
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) rgb += __shfl_xor(rgb, o);
-    if (lane == 0) {
-      acc += rgb / 3u * prefix_len_rgb;
-      const uint32_t last = a.tile_last[t];
-      if (last != NONE) {
-        const uint64_t run = (uint64_t)a.tile_next[t] - last - 1;
-        if (run > 0) {
-          uint64_t m = run - 1;
-          while (true) {
-            acc += lens[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)];
-            if (m < 8) break;
-            m >>= 3;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-    if (lane == 0) a.tile_bits[t] = acc;
   }
 }
 
@@ -1429,6 +1387,7 @@ __global__ __launch_bounds__(256) void enc_tilebits_hist(EncArgs a) {
 __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   __shared__ unsigned long long part[1024];
   const uint32_t g = blockIdx.x, f = blockIdx.y;
+  if (!long_path(a, f)) return;
   const uint32_t g0 = g * ENC_GROUP_TILES;
   const uint32_t nt = min(a.tile_hi - a.tile_lo - g0, ENC_GROUP_TILES);
   const uint64_t base = (uint64_t)f * a.tiles_per_frame + a.tile_lo + g0;
@@ -1467,139 +1426,475 @@ __global__ __launch_bounds__(1024) void enc_tilescan(EncArgs a) {
   }
 }
 
-__global__ __launch_bounds__(ENC_THREADS, 5) void enc_pack(EncArgs a) {
-  __shared__ uint32_t tbl[N_BINS];
+// The packer's tables of frame f (nice_rec.hpp).  An entry composes the codes
+// of its symbols in emission order; entries whose symbols all occur in the
+// frame must fit 32 bits with every code <= FAST_MAX_CODE_BITS, else the frame
+// is FLAG_LONG (entries of absent symbols are never looked up).
+__global__ __launch_bounds__(256) void enc_packtab(EncArgs a) {
+  __shared__ uint32_t code[N_BINS];
+  __shared__ uint8_t len[N_BINS], pres[N_BINS];
+  __shared__ uint32_t s_long;
+  const uint32_t f = blockIdx.x;
+  if (a.frame_flags[f] & FLAG_LONG) return;
+  const int tid = threadIdx.x;
+  for (int b = tid; b < N_BINS; b += 256) {
+    const uint64_t e = (uint64_t)f * N_BINS + b;
+    code[b] = a.tbl_code[e];
+    len[b] = a.tbl_len8[e];
+    pres[b] = a.hist[e] != 0;
+  }
+  if (tid == 0) s_long = 0;
+  __syncthreads();
+  PackTab* out = reinterpret_cast<PackTab*>(a.packtab) + f;
+  bool lng = false;
+  // symbols b[k0 .. n) composed; presence from the payload symbols b[p0 .. n)
+  auto ent = [&](const uint32_t* b, uint32_t k0, uint32_t n, uint32_t p0) -> uint2 {
+    uint32_t L = 0, mx = 0;
+    bool present = true;
+    for (uint32_t k = k0; k < n; ++k) {
+      L += len[b[k]];
+      mx = max(mx, (uint32_t)len[b[k]]);
+      if (k >= p0) present = present && pres[b[k]];
+    }
+    if (present && (L > 32u || mx > (uint32_t)FAST_MAX_CODE_BITS)) lng = true;
+    if (L > 32u || mx > (uint32_t)FAST_MAX_CODE_BITS) return make_uint2(0u, 0u);
+    uint64_t c = 0;
+    for (uint32_t k = k0; k < n; ++k) c = (c << len[b[k]]) | code[b[k]];
+    return make_uint2((uint32_t)c, L);
+  };
+  for (uint32_t e = tid; e < C0_N; e += 256) {
+    uint32_t b[5];
+    const uint32_t n = rec2_syms((e << 3) | rec2_abs(0), b);
+    // T0: the prefix and c0's symbols (LUMA: k and g)
+    out->t0[e] = n ? ent(b, 0, n == 5 ? 3u : 2u, 1) : make_uint2(0u, 0u);
+  }
+  for (uint32_t s = tid; s < SX_N; s += 256) {
+    uint32_t b1 = 0, b2 = 0;
+    const bool live = s < SX_ABS;
+    if (s < SX_L2) { b1 = s; b2 = s; }
+    else if (s < SX_LUMA) { b1 = BIN_LUMA2_R + (s - SX_L2); b2 = BIN_LUMA2_B + (s - SX_L2); }
+    else { b1 = BIN_LUMA_OTHER + (s - SX_LUMA); b2 = b1; }
+    out->t1[s] = live ? ent(&b1, 0, 1, 0) : make_uint2(0u, 0u);
+    out->t2[s] = live ? ent(&b2, 0, 1, 0) : make_uint2(0u, 0u);
+  }
+  for (uint32_t m = tid; m < RC_N; m += 256) {
+    uint32_t b[2];
+    uint32_t n = 0;
+    if (m < RC_TWO) {   // natural digits of m (code.rs:391-406)
+      b[n++] = BIN_PREFIX + P_RUN1 + (m & 7u);
+      if (m >= 8) b[n++] = BIN_PREFIX + P_RUN1 + (m >> 3);
+    } else if (m < RC_NONE) {   // the first two digits of a run of >= 65
+      b[n++] = BIN_PREFIX + P_RUN1 + ((m - RC_TWO) & 7u);
+      b[n++] = BIN_PREFIX + P_RUN1 + ((m - RC_TWO) >> 3);
+    }
+    out->rc[m] = n ? ent(b, 0, n, 0) : make_uint2(0u, 0u);
+  }
+  if (lng) atomicOr(&s_long, 1u);
+  __syncthreads();
+  if (tid == 0 && s_long) {
+    atomicOr(&a.frame_flags[f], FLAG_LONG);
+    atomicOr(&a.frame_flags[a.n_frames], FLAG_LONG);
+  }
+}
+
+// Tile status words of the decoupled look-back (pack_mode 0): the tile's bit
+// count (ST_AGG) as soon as it is known, then its absolute end bit (ST_INCL).
+constexpr unsigned long long ST_AGG = 1ull << 62, ST_INCL = 2ull << 62, ST_VAL = (1ull << 62) - 1;
+__device__ __forceinline__ void st_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long st_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One wave: publishes the tile's count, sums the counts of the tiles before
+// it back to the nearest one whose end is known (or to the frame start,
+// `base`), publishes its own end; returns the tile's start bit.  w: the tile's
+// status index; k: the tiles before it in its frame.  Every tile waited on
+// was claimed earlier by a running block, which never waits on a later one.
+__device__ unsigned long long lookback(unsigned long long* st, uint32_t w, uint32_t k, unsigned long long base,
+                                       uint32_t bits, int lane) {
+  if (k == 0) {
+    if (lane == 0) st_store(&st[w], ST_INCL | (base + bits));
+    return base;
+  }
+  if (lane == 0) st_store(&st[w], ST_AGG | bits);
+  unsigned long long excl = 0;
+  uint32_t j = w - 1, rem = k;
+  while (true) {
+    const bool valid = (uint32_t)lane < rem;
+    const unsigned long long v = valid ? st_load(&st[j - lane]) : 0ull;
+    const uint32_t state = (uint32_t)(v >> 62);
+    const unsigned long long inc = __ballot(valid && state == 2u);
+    const unsigned long long notready = __ballot(valid && state == 0u);
+    const int first = inc ? (int)__builtin_ctzll(inc) : 64;
+    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+    if (notready & need) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    unsigned long long x = (valid && lane <= first) ? (v & ST_VAL) : 0ull;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    excl += x;
+    if (inc) break;
+    if (rem <= 64) { excl += base; break; }
+    j -= 64;
+    rem -= 64;
+  }
+  if (lane == 0) st_store(&st[w], ST_INCL | (excl + bits));
+  return excl;
+}
+
+// Work distribution of enc_pack (wave 0 of a block; f = NONE: no work left).
+// Per-frame tile counters: block b serves slot b % I (I = pack_slots <= 64):
+// frames slot, slot + I, ..., each frame's tiles claimed in order, then any
+// frame with tiles left (scanned 64 counters at a time).  A frame is worked
+// by about G / I blocks at once, so a look-back rarely reaches past one
+// 64-tile window; a tile is claimed only when its block is about to pack it
+// (the next claim goes out once this tile's offset is published), so every
+// tile a look-back waits on publishes its count within one tile's time.
+// pre: the result of a claim on f already issued by the caller (NONE: none).
+__device__ void pack_next(const EncArgs& a, uint32_t nt, uint32_t I, uint32_t slot, uint32_t& f, uint32_t& k,
+                          uint32_t& seq, int lane, uint32_t pre = NONE) {
+  const uint32_t F = a.n_frames;
+  while (true) {
+    if (f != NONE) {
+      uint32_t kk = pre;
+      if (pre == NONE) {
+        if (lane == 0) kk = atomicAdd(&a.pack_ctr[f], 1u);
+        kk = (uint32_t)__shfl((int)kk, 0);
+      }
+      pre = NONE;
+      if (kk < nt) { k = kk; return; }
+    }
+    const uint32_t own = slot + seq * I;
+    if (own < F) {
+      ++seq;
+      f = (a.frame_flags[own] & FLAG_LONG) ? NONE : own;   // long frames: enc_pack_long
+      continue;
+    }
+    f = NONE;
+    for (uint32_t b0 = 0; b0 < F; b0 += 64) {
+      const uint32_t g = b0 + (uint32_t)lane;
+      const bool cand = g < F && !(a.frame_flags[g] & FLAG_LONG) &&
+                        __hip_atomic_load(&a.pack_ctr[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nt;
+      const unsigned long long m = __ballot(cand);
+      if (m) { f = b0 + (uint32_t)__builtin_ctzll(m); break; }
+    }
+    if (f == NONE) return;
+  }
+}
+
+// The thread's 4 pixels of one tile: each pixel's codes (T0, T1, T2, run
+// digits) composed into one value when they fit 32 bits, their bit count, the
+// run digits past a long run's first two, and the thread's total.
+struct QuadCodes {
+  uint32_t v[4], tot[4], xm[4], ri[4], nb, tmax;
+};
+__device__ __forceinline__ uint2 pt_entry(const PackTab& tab, uint32_t r, int i) {
+  // 8-byte entries at the record's field offsets (nice_rec.hpp: bits 3..13,
+  // 14..22, 23..31)
+  const char* tb = reinterpret_cast<const char*>(&tab);
+  return i == 0 ? *reinterpret_cast<const uint2*>(tb + offsetof(PackTab, t0) + (r & 0x3FF8u))
+       : i == 1 ? *reinterpret_cast<const uint2*>(tb + offsetof(PackTab, t1) + ((r >> 11) & 0xFF8u))
+                : *reinterpret_cast<const uint2*>(tb + offsetof(PackTab, t2) + ((r >> 20) & 0xFF8u));
+}
+__device__ __forceinline__ void quad_codes(const PackTab& tab, const uint32_t* mask, int64_t start, int count, int p0,
+                                           uint32_t next_tile_px, const TileQuad& Q, QuadCodes& C) {
+  uint32_t run[4];
+  quad_runs(mask, start, count, p0, next_tile_px, Q, run);
+  C.nb = 0;
+  C.tmax = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t r = Q.rc[q];
+    const uint2 e0 = pt_entry(tab, r, 0), e1 = pt_entry(tab, r, 1), e2 = pt_entry(tab, r, 2);
+    const uint32_t m = run[q] - 1u;
+    C.ri[q] = run[q] == 0 ? RC_NONE : m < 64u ? m : RC_TWO + (m & 63u);
+    const uint2 e3 = tab.rc[C.ri[q]];
+    C.xm[q] = run[q] > 64u ? m >> 6 : 0u;
+    C.tot[q] = e0.y + e1.y + e2.y + e3.y;
+    // composed value, exact when tot <= 32 (shifts stay below 32 then)
+    uint32_t v = e0.x;
+    v = (v << (e1.y & 31u)) | e1.x;
+    v = (v << (e2.y & 31u)) | e2.x;
+    v = (v << (e3.y & 31u)) | e3.x;
+    C.v[q] = v;
+    C.tmax = max(C.tmax, C.tot[q]);
+    C.nb += C.tot[q];
+  }
+  if (C.xm[0] | C.xm[1] | C.xm[2] | C.xm[3]) {   // run digits past a long run's first two (runs of >= 65)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      for (uint32_t xr = C.xm[q]; xr;) {
+        C.nb += tab.rc[xr & 7u].y;
+        if (xr < 8) break;
+        xr >>= 3;
+      }
+    }
+  }
+}
+// Every code of the thread's pixels, in order, through put(val, n) (n <= 32
+// bits of val, 0 when n == 0): one put per pixel when every pixel of the wave
+// fits 32 bits (the common case), else two (the entries read again), else one
+// per entry.
+template <class Put>
+__device__ __forceinline__ void quad_emit(const PackTab& tab, const TileQuad& Q, const QuadCodes& C, Put&& put) {
+  auto put_extra = [&](uint32_t xr) {
+    while (true) {
+      const uint2 d = tab.rc[xr & 7u];
+      put(d.x, d.y);
+      if (xr < 8) break;
+      xr >>= 3;
+    }
+  };
+  if (__all(C.tmax <= 32u)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      put(C.v[q], C.tot[q]);
+      if (C.xm[q]) put_extra(C.xm[q]);
+    }
+  } else if (__all(C.tmax <= 64u)) {
+    for (int q = 0; q < 4; ++q) {
+      const uint2 e0 = pt_entry(tab, Q.rc[q], 0), e1 = pt_entry(tab, Q.rc[q], 1), e2 = pt_entry(tab, Q.rc[q], 2);
+      const uint2 e3 = tab.rc[C.ri[q]];
+      uint64_t v = e0.x;
+      v = (v << e1.y) | e1.x;
+      v = (v << e2.y) | e2.x;
+      v = (v << e3.y) | e3.x;
+      const bool two = C.tot[q] > 32u;
+      put(two ? (uint32_t)(v >> 32) : 0u, two ? C.tot[q] - 32u : 0u);
+      put((uint32_t)v, two ? 32u : C.tot[q]);
+      if (C.xm[q]) put_extra(C.xm[q]);
+    }
+  } else {
+    for (int q = 0; q < 4; ++q) {
+      for (int i = 0; i < 3; ++i) {
+        const uint2 e = pt_entry(tab, Q.rc[q], i);
+        put(e.x, e.y);
+      }
+      const uint2 e3 = tab.rc[C.ri[q]];
+      put(e3.x, e3.y);
+      if (C.xm[q]) put_extra(C.xm[q]);
+    }
+  }
+}
+
+// One work item of enc_pack is PACK_SUB consecutive tiles of a frame (a
+// "group"): one claim and one look-back per 4096 pixels.  The group's codes
+// go into the LDS bit buffer tile by tile; its status word, offset and edge
+// word are those of its first tile.  A group of over PACK_CAP_BITS bits (over
+// 32 bits per pixel on average) is counted first and then OR-ed into the
+// output directly.
+__global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
+  __shared__ PackTab tab;
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
-  __shared__ uint32_t wsum[ENC_THREADS / 64];
-  __shared__ RecBinTable rbt;
-  rbt_init(rbt, threadIdx.x);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ uint32_t wsum[PK_THREADS / 64];
+  __shared__ uint32_t s_f, s_k;
+  __shared__ unsigned long long s_off;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;   // groups per frame
   const uint32_t T = a.tiles_per_frame;
-  const uint64_t total = (uint64_t)a.n_frames * T;
   const int64_t N = (int64_t)a.W * a.H;
-  const int p0 = 4 * threadIdx.x;
-  uint32_t cur_f = 0xFFFFFFFFu;
-  uint32_t used_words = PACK_MAX_WORDS;
-  uint64_t t0, t1;
-  tile_range(a, t0, t1);
-  (void)total;
-  uint32_t rn[4];
-  TileIter it(a, t0), nx(a, t0);
-  if (t0 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
-  for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
-    const uint64_t t = it.tile();
-    uint32_t rc[4] = {rn[0], rn[1], rn[2], rn[3]};
-    nx.step(1);
-    if (w + 1 < t1) quad_fetch(a, nx.f, nx.tt(), p0, rn);
-    const uint32_t f = it.f, tt = it.tt();
-    if (a.frame_flags[f] & FLAG_LONG) continue;   // enc_pack_long's frame (block-uniform)
-    const int64_t start = (int64_t)tt * ENC_TILE;
-    const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
-    __syncthreads();
-    for (uint32_t w = threadIdx.x; w < used_words; w += ENC_THREADS) bits[w] = 0;
-    if (f != cur_f) { load_tbl(tbl, a, f); cur_f = f; }
-    TileQuad Q;
-    quad_mask(rc, lane, wid, mask, Q);
-    __syncthreads();
-    quad_bits(tbl, rbt, mask, start, count, p0, a.tile_next[t], Q);
-    const uint32_t x = wave_incl_scan(Q.nb);
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    uint32_t wbase = 0, tile_bits = 0;
-#pragma unroll
-    for (int w = 0; w < ENC_THREADS / 64; ++w) {
-      const uint32_t ws = wsum[w];
-      wbase += (w < wid) ? ws : 0u;
-      tile_bits += ws;
+  const int p0 = 4 * tid;
+  const bool lookback_mode = a.pack_mode == 0;
+  const uint32_t I = a.pack_slots, slot = blockIdx.x % a.pack_slots;
+  uint32_t cf = NONE, ck = 0, seq = 0;   // wave 0's work cursor
+#ifdef NICE_PACK_PROF
+  long long pr[7] = {0, 0, 0, 0, 0, 0, 0}, pt = clock64(), pn = 0;
+#define PROF_MARK(i) do { const long long c_ = clock64(); pr[i] += c_ - pt; pt = c_; } while (0)
+#else
+#define PROF_MARK(i) do {} while (0)
+#endif
+  if (wid == 0) {
+    pack_next(a, ng, I, slot, cf, ck, seq, lane);
+    if (lane == 0) { s_f = cf; s_k = ck; }
+  }
+  __syncthreads();
+  uint32_t f = s_f, g = s_k;
+  uint32_t cur_f = NONE, used_words = PACK_MAX_WORDS;
+  while (f != NONE) {
+    const uint32_t k0 = g * PACK_SUB, nsub = min((uint32_t)PACK_SUB, nt - k0);
+    const uint32_t tt0 = a.tile_lo + k0;
+    const uint64_t t0 = (uint64_t)f * T + tt0;   // the group's first tile
+    if (f != cur_f) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.packtab + (uint64_t)f * sizeof(PackTab));
+      uint4* dst = reinterpret_cast<uint4*>(&tab);
+      for (int i = tid; i < (int)(sizeof(PackTab) / 16); i += PK_THREADS) dst[i] = src[i];
+      cur_f = f;
     }
-    if (Q.nb) {
-      uint32_t pp = wbase + x - Q.nb;   // the lane's next bit in the tile
-      // n <= 32 bits of val (0 when n == 0) at bit pp, MSB-first: one 64-bit
-      // shift places them across words pp >> 5 and pp >> 5 + 1, both OR-ed
-      // into LDS (words shared with neighbouring lanes).  No accumulator
-      // carried from put to put, so a lane's puts are independent (measured:
-      // the accumulator version's flush selects were ~14 VALU per put).
-      auto put_n = [&](uint32_t val, uint32_t n) {
-        const uint32_t s = pp & 31u, w = pp >> 5;
-        const uint64_t v = (uint64_t)val << ((64u - s - n) & 63u);
-        atomicOr(&bits[w], (uint32_t)(v >> 32));
-        atomicOr(&bits[w + 1], (uint32_t)v);
-        pp += n;
-      };
-      auto put = [&](uint32_t e) { put_n(e >> 5, e & 31u); };   // e == 0: no symbol
-      // a pixel's codes composed into one value: 32 bits for every pixel of
-      // the wave (the common case: one put per pixel), else 64 bits (two
-      // puts), else one put per code
-      uint32_t tot[4];
-      uint32_t tmax = 0;
+    for (uint32_t i = tid; i < used_words; i += PK_THREADS) bits[i] = 0;
+    uint32_t rc[4], rn[4];
+    quad_fetch(a, f, tt0, p0, rc);
+    uint32_t gbits = 0;   // the group's bits so far (block-uniform)
+    bool over = false;
+    for (uint32_t s = 0; s < nsub; ++s) {
+      const uint32_t tt = tt0 + s;
+      const int64_t start = (int64_t)tt * ENC_TILE;
+      const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+      if (s + 1 < nsub) quad_fetch(a, f, tt + 1, p0, rn);
+      TileQuad Q;
+      quad_mask(rc, lane, wid, mask, Q);
+      __syncthreads();
+      PROF_MARK(0);
+      QuadCodes C;
+      quad_codes(tab, mask, start, count, p0, a.tile_next[(uint64_t)f * T + tt], Q, C);
+      const uint32_t x = wave_incl_scan(C.nb);
+      if (lane == 63) wsum[wid] = x;
+      __syncthreads();
+      uint32_t wbase = 0, sbits = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        tot[q] = (Q.e[q][0] & 31u) + (Q.e[q][1] & 31u) + (Q.e[q][2] & 31u) + (Q.e[q][3] & 31u) + (Q.e[q][4] & 31u);
-        tmax = max(tmax, tot[q]);
+      for (int i = 0; i < PK_THREADS / 64; ++i) {
+        const uint32_t ws = wsum[i];
+        wbase += (i < wid) ? ws : 0u;
+        sbits += ws;
       }
-      auto put_runs = [&](int q) {
-        if (Q.run[q] > 0) {
-          uint64_t m = Q.run[q] - 1;
-          while (true) {
-            put(tbl[BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u)]);
-            if (m < 8) break;
-            m >>= 3;
-          }
-        }
-      };
-      if (__all(tmax <= 32u)) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t v = 0;
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const uint32_t e = Q.e[q][k];
-            v = (v << (e & 31u)) | (e >> 5);
-          }
-          put_n(v, tot[q]);
-          put_runs(q);
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (tot[q] <= 64u) {
-            uint64_t v = 0;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-              const uint32_t e = Q.e[q][k], n = e & 31u;
-              v = (v << n) | (e >> 5);
-            }
-            const bool two = tot[q] > 32u;
-            put_n(two ? (uint32_t)(v >> 32) : 0u, two ? tot[q] - 32u : 0u);
-            put_n((uint32_t)v, two ? 32u : tot[q]);
-          } else {
-            put(Q.e[q][0]);
-            put(Q.e[q][1]);
-            put(Q.e[q][2]);
-            put(Q.e[q][3]);
-            put(Q.e[q][4]);
-          }
-          put_runs(q);
-        }
+      PROF_MARK(1);
+      over = over || gbits + sbits > (uint32_t)PACK_CAP_BITS;
+      if (!over && C.nb) {
+        // at bit pp, MSB-first: one 64-bit shift places the bits across
+        // words pp >> 5 and pp >> 5 + 1, both OR-ed into LDS (words shared
+        // with neighbouring lanes)
+        uint32_t pp = gbits + wbase + x - C.nb;
+        quad_emit(tab, Q, C, [&](uint32_t val, uint32_t n) {
+          const uint32_t sh = pp & 31u, wd = pp >> 5;
+          const uint64_t v = (uint64_t)val << ((64u - sh - n) & 63u);
+          atomicOr(&bits[wd], (uint32_t)(v >> 32));
+          atomicOr(&bits[wd + 1], (uint32_t)v);
+          pp += n;
+        });
       }
+      PROF_MARK(2);
+      gbits += sbits;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rc[q] = rn[q];
+      __syncthreads();   // wsum and mask are rewritten by the next tile
+    }
+    if (wid == 0 && lookback_mode) {
+      const unsigned long long off = lookback(a.status, f * ng + g, g, a.seed_bit[f], gbits, lane);
+      if (lane == 0) s_off = off;
     }
     __syncthreads();
-    // place the tile's bits at its stream offset
-    const uint64_t s0 = a.tile_off[t], e0 = s0 + tile_bits;
+    PROF_MARK(3);
+    // place the group's bits at its stream offset
+    const unsigned long long s0 = lookback_mode ? s_off : a.tile_off[t0], e0 = s0 + gbits;
     const uint32_t sh = (uint32_t)(s0 & 31);
     const uint64_t w0 = s0 >> 5;
-    const uint32_t nw = tile_bits ? (uint32_t)(((e0 + 31) >> 5) - w0) : 0u;
+    const uint32_t nw = gbits ? (uint32_t)(((e0 + 31) >> 5) - w0) : 0u;
     uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
-    for (uint32_t m = threadIdx.x; m < nw; m += ENC_THREADS) {
-      const uint32_t hi = m ? bits[m - 1] : 0u;
-      const uint32_t lo = bits[m];   // zero past the tile's bits
-      const uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
-      const bool shared = (m == 0 && sh) || (m == nw - 1 && (e0 & 31));
-      if (shared) atomicOr(&out32[w0 + m], __builtin_bswap32(v));
-      else out32[w0 + m] = __builtin_bswap32(v);
+    if (!over) {
+      for (uint32_t m = tid; m < nw; m += PK_THREADS) {
+        const uint32_t hi = m ? bits[m - 1] : 0u;
+        const uint32_t lo = bits[m];   // zero past the group's bits
+        const uint32_t v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+        if (lookback_mode) {
+          // a word is stored by the group holding its first bit (zeros past
+          // the group's end); this group's bits in the word holding its
+          // start go to enc_edges
+          if (m == 0 && sh) a.tile_bits[t0] = v;
+          else out32[w0 + m] = __builtin_bswap32(v);
+        } else {   // every partial word was zeroed by enc_tilescan
+          const bool shared = (m == 0 && sh) || (m == nw - 1 && (e0 & 31));
+          if (shared) atomicOr(&out32[w0 + m], __builtin_bswap32(v));
+          else out32[w0 + m] = __builtin_bswap32(v);
+        }
+      }
+    } else {
+      // zero the words only this group writes (look-back: every word whose
+      // first bit is the group's; bands: the interior ones, enc_tilescan
+      // zeroed the partial ones), then OR each code into place, tile by tile
+      const uint64_t z0 = (s0 + 31) >> 5, z1 = lookback_mode ? (e0 + 31) >> 5 : e0 >> 5;
+      for (uint64_t m = z0 + tid; m < z1; m += PK_THREADS) out32[m] = 0u;
+      if (lookback_mode && tid == 0) a.tile_bits[t0] = 0u;
+      __threadfence();
+      __syncthreads();
+      auto or_word = [&](uint64_t wd, uint32_t v) {
+        if (!v) return;
+        if (lookback_mode && sh && wd == w0) atomicOr(&a.tile_bits[t0], v);
+        else atomicOr(&out32[wd], __builtin_bswap32(v));
+      };
+      unsigned long long run = s0;
+      for (uint32_t s = 0; s < nsub; ++s) {
+        const uint32_t tt = tt0 + s;
+        const int64_t start = (int64_t)tt * ENC_TILE;
+        const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+        quad_fetch(a, f, tt, p0, rc);
+        TileQuad Q;
+        quad_mask(rc, lane, wid, mask, Q);
+        __syncthreads();
+        QuadCodes C;
+        quad_codes(tab, mask, start, count, p0, a.tile_next[(uint64_t)f * T + tt], Q, C);
+        const uint32_t x = wave_incl_scan(C.nb);
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        uint32_t wbase = 0, sbits = 0;
+#pragma unroll
+        for (int i = 0; i < PK_THREADS / 64; ++i) {
+          const uint32_t ws = wsum[i];
+          wbase += (i < wid) ? ws : 0u;
+          sbits += ws;
+        }
+        if (C.nb) {
+          unsigned long long pp = run + wbase + x - C.nb;
+          quad_emit(tab, Q, C, [&](uint32_t val, uint32_t n) {
+            const uint32_t b = (uint32_t)(pp & 31u);
+            const uint64_t v = (uint64_t)val << ((64u - b - n) & 63u);
+            if (n) {
+              or_word(pp >> 5, (uint32_t)(v >> 32));
+              or_word((pp >> 5) + 1, (uint32_t)v);
+            }
+            pp += n;
+          });
+        }
+        run += sbits;
+        __syncthreads();
+      }
     }
-    used_words = nw + 1;
+    if (lookback_mode && tid == 0) {
+      a.tile_off[t0] = s0;
+      if (!over && !(nw && sh)) a.tile_bits[t0] = 0u;
+      if (tt0 + nsub == T) a.data_end[f] = e0;
+    }
+    used_words = over ? 0u : nw + 1;
+    PROF_MARK(4);
+    // the next group: claimed only now, when this block can start it at once
+    // (a group claimed earlier would keep the look-backs of the groups after
+    // it waiting while its block finishes this one)
+    if (wid == 0) {
+      pack_next(a, ng, I, slot, cf, ck, seq, lane);
+      if (lane == 0) { s_f = cf; s_k = ck; }
+    }
+    __syncthreads();
+    f = s_f;
+    g = s_k;
+    PROF_MARK(5);
+#ifdef NICE_PACK_PROF
+    ++pn;
+#endif
+  }
+#ifdef NICE_PACK_PROF
+  if (tid == 0 && (blockIdx.x % 256) == 0)
+    printf("enc_pack block %u: groups %lld cycles/group: wait+mask %lld codes+scan %lld puts %lld lookback %lld "
+           "place %lld claim %lld\n", blockIdx.x, pn, pr[0] / max(pn, 1ll), pr[1] / max(pn, 1ll),
+           pr[2] / max(pn, 1ll), pr[3] / max(pn, 1ll), pr[4] / max(pn, 1ll), pr[5] / max(pn, 1ll));
+#endif
+}
+
+// Each group's bits in the word holding its first bit (pack_mode 0), OR-ed
+// into that word once every group has stored its own words.
+__global__ __launch_bounds__(256) void enc_edges(EncArgs a) {
+  const uint32_t T = a.tiles_per_frame;
+  const uint32_t ng = (T + PACK_SUB - 1) / PACK_SUB;
+  for (uint32_t f = blockIdx.y; f < a.n_frames; f += gridDim.y) {
+    if (a.frame_flags[f] & FLAG_LONG) continue;
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
+    for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < ng; g += gridDim.x * 256) {
+      const uint64_t t = (uint64_t)f * T + (uint64_t)g * PACK_SUB;
+      const uint32_t e = a.tile_bits[t];
+      if (e) atomicOr(&out32[a.tile_off[t] >> 5], __builtin_bswap32(e));
+    }
   }
 }
 
@@ -1658,9 +1953,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
   __shared__ uint32_t lens[N_BINS];
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t wsum[ENC_THREADS / 64];
-  __shared__ RecBinTable rbt;
   if (!(a.frame_flags[a.n_frames] & FLAG_LONG)) return;   // no long-code frame in the batch
-  rbt_init(rbt, threadIdx.x);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t N = (int64_t)a.W * a.H;
   const int p0 = 4 * threadIdx.x;
@@ -1687,7 +1980,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
     TileQuad Q;
     quad_mask(rc, lane, wid, mask, Q);
     __syncthreads();
-    const uint32_t nb = quad_nbits(lens, rbt, mask, start, count, p0, a.tile_next[t], Q);
+    const uint32_t nb = quad_nbits(lens, mask, start, count, p0, a.tile_next[t], Q);
     const uint32_t x = wave_incl_scan(nb);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
@@ -1727,24 +2020,17 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
       }
       pos += n;
     };
-    const int nx_local = next_coded_local(mask, p0 + 3);
-    const uint64_t after = (nx_local < count) ? (uint64_t)(start + nx_local) : (uint64_t)a.tile_next[t];
+    uint32_t run[4];
+    quad_runs(mask, start, count, p0, a.tile_next[t], Q, run);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (!((Q.nib >> q) & 1u)) continue;
-      uint32_t b0, b1, b2, b3;
-      const uint32_t n = rec_bins(rbt, Q.rc[q], b0, b1, b2, b3);
-      emit(BIN_PREFIX + min(Q.rc[q] & 7u, 4u));
-      emit(b0);
-      if (n > 1) { emit(b1); emit(b2); }
-      if (n > 3) emit(b3);
-      const uint32_t later = Q.nib >> (q + 1);
-      const uint64_t nxt = later ? (uint64_t)(start + p0 + q + 1 + __builtin_ctz(later)) : after;
-      const uint64_t run = nxt - (uint64_t)(start + p0 + q) - 1;
-      if (run > 0) {
-        uint64_t m = run - 1;
+      uint32_t b[5];
+      const uint32_t n = rec2_syms(Q.rc[q], b);
+      for (uint32_t k = 0; k < n; ++k) emit(b[k]);
+      if (run[q] > 0) {
+        uint32_t m = run[q] - 1;
         while (true) {
-          emit(BIN_PREFIX + P_RUN1 + (uint32_t)(m & 7u));
+          emit(BIN_PREFIX + P_RUN1 + (m & 7u));
           if (m < 8) break;
           m >>= 3;
         }

@@ -39,9 +39,15 @@ struct EncArgs {
   uint8_t* hdr_bitoff;       // n_frames
   uint32_t* recs;            // n_frames * rec_stride per-pixel symbol records
   uint64_t rec_stride;       // W*H rounded up to 4
-  uint32_t* tile_hist;       // n_frames * T * TH_WORDS: per-tile symbol counts, u16 pairs (ring path), else null
-  uint32_t* tile_bits;       // n_frames * T: data bits per tile
+  uint32_t* tile_bits;       // n_frames * T: data bits per tile (long path); pack_mode 0: the
+                             // tile's bits in the word holding its first bit (enc_edges)
   unsigned long long* tile_off;   // n_frames * T: absolute bit offset of each tile
+  uint8_t* packtab;          // n_frames * sizeof(PackTab): the packer's code tables (nice_rec.hpp)
+  uint32_t* pack_ctr;        // n_frames: enc_pack's per-frame tile counters (zeroed per launch)
+  uint32_t pack_slots;       // enc_pack: frames worked at once (blocks per frame = grid / slots)
+  unsigned long long* status;   // n_frames * (tile_hi - tile_lo): look-back status words (zeroed per launch)
+  uint32_t pack_mode;        // 0: tile offsets by look-back (frames); 1: from enc_tilescan (bands)
+  uint32_t long_only;        // 1: enc_tilebits / enc_tilescan serve FLAG_LONG frames only
   unsigned long long* data_end;   // n_frames: bit position after the last data bit
   // Band mode (one image sharded over ranks): only tiles
   // [tile_lo, tile_hi) of each frame are processed; pixel memory is valid for
@@ -63,7 +69,8 @@ constexpr uint32_t ENC_GROUP_TILES = 8192;
 
 __global__ void enc_classify(EncArgs a);        // W >= 3
 __global__ void enc_classify_tiny(EncArgs a);   // W < 3
-__global__ void enc_classify_ring(EncArgs a);
+__global__ void enc_classify_ring(EncArgs a);    // RGBA
+__global__ void enc_classify_ring3(EncArgs a);   // RGB, 4-byte aligned frames
 // the 16K-pixel ring holds 3W + 3 pixels of references plus two tiles (the one
 // being classified and the next one being staged): 3W + 3 + 2048 <= 16384
 constexpr uint32_t CLS_RING_MAX_W = 4777;
@@ -75,12 +82,13 @@ __global__ void enc_tables(EncArgs a);
 __global__ void enc_code_lengths_test(const uint32_t* counts, int n, uint8_t* aob);
 __global__ void enc_header(EncArgs a);
 __global__ void enc_tilebits(EncArgs a);
-__global__ void enc_tilebits_hist(EncArgs a);
-constexpr uint32_t TH_WORDS = 432;   // u32 words per tile histogram (858 u16 counts, 16-B aligned rows)
 __global__ void enc_tilescan(EncArgs a);
 // group aggregates for the tile scans: what 0 = min of tile_first, 1 = sum of tile_bits
 __global__ void enc_group_reduce(EncArgs a, int what);
+__global__ void enc_packtab(EncArgs a);
 __global__ void enc_pack(EncArgs a);
+__global__ void enc_edges(EncArgs a);
+constexpr uint32_t PACK_BLOCKS_PER_CU = 4;   // enc_pack: 256 threads, ~35 KB LDS
 __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
 __global__ void enc_band_sum(EncArgs a, unsigned long long* info);
