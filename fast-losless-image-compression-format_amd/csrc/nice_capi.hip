@@ -275,6 +275,18 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
 }
 }  // namespace
 
+// enc_classify_strip: rows per block (about three blocks per CU over all
+// frames and strips, >= 16 rows so the 3-row prefill stays small) and the grid
+static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, uint32_t rows_total, uint32_t* blocks) {
+  const uint64_t strips = (w + STRIP_W_HOST - 1) / STRIP_W_HOST;
+  const uint64_t want = 3ull * (uint64_t)ctx->cus;
+  uint64_t r = (rows_total * strips * n_frames + want - 1) / want;
+  if (r < 16) r = 16;
+  if (r > rows_total) r = rows_total ? rows_total : 1;
+  *blocks = (uint32_t)(n_frames * strips * ((rows_total + r - 1) / r));
+  return (uint32_t)r;
+}
+
 extern "C" {
 
 int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t frame_stride,
@@ -296,6 +308,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   const uint32_t T = tiles_for(w, h);
   const bool aligned = ((uintptr_t)d_px & 3) == 0 && (frame_stride & 3) == 0;
   const bool ring = aligned && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
+  const bool strip = aligned && channels == 4 && w > CLS_RING_MAX_W && w % ENC_TILE == 0 && !getenv("NICE_ENC_NO_RING");
   if ((uint64_t)n_frames * T >= (1ull << 32)) return NICE_E_ARG;   // enc_pack's 32-bit work counter
   EncLayout L = enc_layout(n_frames, T, N);
   int rc = ctx->enc.grow(L.total);
@@ -322,7 +335,11 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     a.tiles_per_block = (uint32_t)per;
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
-    if (ring && channels == 4)
+    if (strip) {
+      uint32_t sblocks;
+      a.tiles_per_block = strip_rows(ctx, n_frames, w, h, &sblocks);
+      hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    } else if (ring && channels == 4)
       hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
     else if (ring)
       hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
@@ -767,7 +784,14 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (per < 1) per = 1;
   blocks = (work + per - 1) / per;
   a.tiles_per_block = (uint32_t)per;
-  if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  if (channels == 4 && w > CLS_RING_MAX_W && w % ENC_TILE == 0 && ((uintptr_t)d_px & 3) == 0 &&
+      !getenv("NICE_ENC_NO_RING")) {
+    // the band's rows in strips (tiles outside the band are staged, not classified)
+    const uint32_t tpr = w / ENC_TILE, rows_band = (tile_hi + tpr - 1) / tpr - tile_lo / tpr;
+    uint32_t sblocks;
+    a.tiles_per_block = strip_rows(ctx, 1, w, rows_band, &sblocks);
+    hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
+  } else if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_band_edges, dim3(1), dim3(256), 0, st, a, d_edges);
   NICE_HIP(hipGetLastError());

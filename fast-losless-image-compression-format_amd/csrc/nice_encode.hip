@@ -514,13 +514,24 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 // the prediction is L and LUMA2 is skipped, SMALL_DIFF and LUMA need i > 0, and
 // the raw residual is taken against 0 at i = 0.  (The back reference to pixel
 // i-1 can never hit a coded pixel, so it is not tested.)
+// The four neighbour groups of the lane's pixel: b0 = pixels i-3 .. i (row y),
+// b1 = row y-1 from 3 left, b2 = pixel i-2W, b3 = row y-3 from 3 left; the
+// hit's difference is read again at rbase[ltab[k] + tid].
+template <bool HEAD>
+__device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
+                                               const uint32_t* b3, const uint32_t* rbase, uint32_t tid, uint32_t W,
+                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd);
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
                                                   uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
-  const uint32_t* b0 = ring + ((s - 3u) & (CLS_RING - 1)) + tid;
-  const uint32_t* b1 = ring + ((s - W - 3u) & (CLS_RING - 1)) + tid;
-  const uint32_t* b2 = ring + ((s - 2u * W) & (CLS_RING - 1)) + tid;
-  const uint32_t* b3 = ring + ((s - 3u * W - 3u) & (CLS_RING - 1)) + tid;
+  return classify_y<HEAD>(ring + ((s - 3u) & (CLS_RING - 1)) + tid, ring + ((s - W - 3u) & (CLS_RING - 1)) + tid,
+                          ring + ((s - 2u * W) & (CLS_RING - 1)) + tid,
+                          ring + ((s - 3u * W - 3u) & (CLS_RING - 1)) + tid, ring, tid, W, i, ltab, cbr, csd);
+}
+template <bool HEAD>
+__device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
+                                               const uint32_t* b3, const uint32_t* rbase, uint32_t tid, uint32_t W,
+                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
   const uint32_t X = b0[3], L2 = b0[1], L3 = b0[0];
   uint32_t L = b0[2];
   const uint32_t U = b1[3], UR1 = b1[4], UR3 = b1[6], UL3 = b1[0];
@@ -577,7 +588,7 @@ __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t
       const uint32_t m = min(min(min(min(key[0], key[1]), key[2]), min(min(key[3], key[4]), key[5])),
                              min(min(min(key[6], key[7]), key[8]), min(key[9], key[10])));
       lk = min(m, 11u);
-      lt = xk - ring[ltab[m & 15u] + tid];
+      lt = xk - rbase[ltab[m & 15u] + tid];
     }
   }
   const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
@@ -815,6 +826,185 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
 }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4>(a); }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3>(a); }
+
+// ---------------------------------------------------------------------------
+// K1s: classify, strip-staged (RGBA frames with W % 1024 == 0 too wide for the
+// ring: W > CLS_RING_MAX_W).  The frame is cut into vertical strips of up to
+// STRIP_W columns (a multiple of 1024, so each strip row is whole raster tiles
+// and the tile bookkeeping is the ring kernel's); a block walks rows
+// [y0, y1) of one strip keeping four row windows in LDS, each the LINEAR
+// pixels [yW + x0 - 3, yW + x1 + 3) of its row: every reference of a pixel
+// of the strip -- 0..3 rows up, 3 pixels either side, wrapping across row ends
+// like the reference's linear offsets (code.rs:141-145) -- is inside the
+// window of its row.  Same outputs as enc_classify_ring.
+// ---------------------------------------------------------------------------
+constexpr int STRIP_W = 2048;
+constexpr int STRIP_RS = STRIP_W + 8;              // window words (+3 each side, padded)
+constexpr int STRIP_LD = (STRIP_W + 6 + CLS_THREADS - 1) / CLS_THREADS;   // window loads per thread (5)
+
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
+  __shared__ uint32_t win[4][STRIP_RS];
+  __shared__ uint32_t hs[C0_N + 2 * SX_N];
+  __shared__ uint32_t run_hist[8];
+  __shared__ uint32_t mask[STRIP_W / ENC_TILE][ENC_TILE / 32];
+  __shared__ uint32_t ltab[STRIP_W / ENC_TILE][CLS_PPT][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t W = a.W, H = a.H;
+  const uint32_t T = a.tiles_per_frame, tpr = W / ENC_TILE;   // tiles per row
+  const uint32_t nstrips = (W + STRIP_W - 1) / STRIP_W;
+  const uint32_t rows = a.tiles_per_block;                    // rows per block
+  // the band's rows (frames: all)
+  const uint32_t ylo = a.tile_lo / tpr, yhi = (a.tile_hi + tpr - 1) / tpr;
+  const uint32_t nchunks = (yhi - ylo + rows - 1) / rows;
+  uint32_t b = blockIdx.x;
+  const uint32_t chunk = b % nchunks;
+  b /= nchunks;
+  const uint32_t s = b % nstrips, f = b / nstrips;
+  if (f >= a.n_frames) return;
+  const uint32_t y0 = ylo + chunk * rows, y1 = min(y0 + rows, yhi);
+  const uint32_t x0 = s * STRIP_W, x1 = min(x0 + STRIP_W, W);
+  const uint32_t ntr = (x1 - x0) / ENC_TILE;                  // tiles per strip row (1 or 2)
+  const uint8_t* fr = a.px + (uint64_t)f * a.frame_stride;
+  const int64_t N = (int64_t)W * H;
+  const uint32_t cbr = (C0_BR << 3) | rec2_abs((uint32_t)lane), csd = (C0_SD << 3) | rec2_abs((uint32_t)lane);
+  const uint32_t cunc = rec2_unc((uint32_t)lane);
+  for (int k = tid; k < (int)(C0_N + 2 * SX_N); k += CLS_THREADS) hs[k] = 0;
+  if (tid < 8) run_hist[tid] = 0;
+  // row y's window: linear pixels [yW + x0 - 3, yW + x1 + 3) (0 outside the
+  // frame / the caller's pixel memory), loaded into registers
+  uint32_t pw[STRIP_LD];
+  auto fetch_row = [&](uint32_t y) {
+    const int64_t g0 = (int64_t)y * W + x0 - 3;
+    const int64_t lo = max((int64_t)0, a.px_lo), hi = min(N, a.px_hi);
+#pragma unroll
+    for (int k = 0; k < STRIP_LD; ++k) {
+      const int c = tid + k * CLS_THREADS;
+      const int64_t g = g0 + c;
+      pw[k] = (c < (int)(x1 - x0) + 6 && g >= lo && g < hi) ? reinterpret_cast<const uint32_t*>(fr)[g] : 0u;
+    }
+  };
+  auto commit_row = [&](uint32_t y) {
+    uint32_t* wr = win[y & 3];
+#pragma unroll
+    for (int k = 0; k < STRIP_LD; ++k) {
+      const int c = tid + k * CLS_THREADS;
+      if (c < (int)(x1 - x0) + 6) wr[c] = y_from_rgba(pw[k]);
+    }
+  };
+  // prefill rows y0-3 .. y0-1
+  for (uint32_t y = y0 >= 3 ? y0 - 3 : 0; y < y0; ++y) {
+    fetch_row(y);
+    commit_row(y);
+  }
+  // back distance of luma reference k in (rows, pixels) for the tile tables
+  const int lk_rows = tid < 16 && tid < 11 ? lr_rows(tid) : 0, lk_px = tid < 16 && tid < 11 ? lr_px(tid) : 0;
+  fetch_row(y0);
+  for (uint32_t y = y0; y < y1; ++y) {
+    // row y's window replaces row y - 4's, which row y - 1 still references:
+    // every thread is past row y - 1 first (also for ltab and mask)
+    __syncthreads();
+    commit_row(y);
+    if (y + 1 < y1) fetch_row(y + 1);
+    // luma reference tables: window index of reference k for thread 0 of
+    // (tile j, q); the window of row y - r holds column x at x - x0 + 3
+    if (tid < 16) {
+      for (uint32_t j = 0; j < ntr; ++j)
+#pragma unroll
+        for (int q = 0; q < CLS_PPT; ++q)
+          ltab[j][q][tid] = ((y - (uint32_t)lk_rows) & 3u) * STRIP_RS +
+                            (uint32_t)((int)(j * ENC_TILE + q * CLS_THREADS) + 3 - lk_px);
+    }
+    __syncthreads();
+    // coded flags of the row's tiles
+    uint32_t coded_bits = 0;
+    unsigned long long wbal[2][CLS_PPT];
+    const uint32_t* wy = win[y & 3];
+    for (uint32_t j = 0; j < ntr; ++j) {
+#pragma unroll
+      for (int q = 0; q < CLS_PPT; ++q) {
+        const int c = (int)(j * ENC_TILE) + q * CLS_THREADS + tid;   // column in the strip
+        const int64_t i = (int64_t)y * W + x0 + c;
+        const bool coded = i == 0 || wy[c + 3] != wy[c + 2];
+        const unsigned long long bal = __ballot(coded);
+        wbal[j][q] = bal;
+        if (lane == 0) {
+          const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
+          mask[j][wb] = (uint32_t)bal;
+          mask[j][wb + 1] = (uint32_t)(bal >> 32);
+        }
+        coded_bits |= (coded ? 1u : 0u) << (2 * j + q);
+      }
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < ntr; ++j) {
+      const uint32_t tt = (y * W + x0) / ENC_TILE + j;   // raster tile
+      const bool in_band = tt >= a.tile_lo && tt < a.tile_hi;   // block-uniform
+      const int64_t start = (int64_t)tt * ENC_TILE;
+      if (in_band && (tid >> 6) == (int)j) {   // first / last coded pixel: wave j
+        const uint32_t mw = lane < ENC_TILE / 32 ? mask[j][lane] : 0u;
+        const unsigned long long nz = __ballot(mw != 0);
+        if (lane == 0) {
+          const uint64_t t = (uint64_t)f * T + tt;
+          uint32_t first = NONE, last = NONE;
+          if (nz) {
+            const int fw = __builtin_ctzll(nz), lw = 63 - __builtin_clzll(nz);
+            first = (uint32_t)(start + fw * 32 + __builtin_ctz(mask[j][fw]));
+            last = (uint32_t)(start + lw * 32 + 31 - __builtin_clz(mask[j][lw]));
+          }
+          a.tile_first[t] = first;
+          a.tile_last[t] = last;
+        }
+      }
+      if (!in_band) continue;
+      const bool fast = start >= 3 * (int64_t)W + 3;
+      uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
+      uint32_t rec[CLS_PPT];
+#pragma unroll
+      for (int q = 0; q < CLS_PPT; ++q) {
+        const int p = q * CLS_THREADS + tid;
+        const uint32_t cs = j * ENC_TILE + q * CLS_THREADS;   // strip column of thread 0
+        const bool coded = (coded_bits >> (2 * j + q)) & 1u;
+        const uint32_t* b0 = win[y & 3] + cs + tid;
+        const uint32_t* b1 = win[(y - 1) & 3] + cs + tid;
+        const uint32_t* b2 = win[(y - 2) & 3] + cs + 3 + tid;
+        const uint32_t* b3 = win[(y - 3) & 3] + cs + tid;
+        uint32_t rf;
+        if (fast)
+          rf = classify_y<false>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, 0u, ltab[j][q], cbr, csd);
+        else
+          rf = classify_y<true>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, (uint32_t)(start + p), ltab[j][q], cbr,
+                                csd);
+        rec[q] = coded ? rf : cunc;
+      }
+#pragma unroll
+      for (int q = 0; q < CLS_PPT; ++q) {
+        const int p = q * CLS_THREADS + tid;
+        const bool coded = (coded_bits >> (2 * j + q)) & 1u;
+        recs[p] = rec[q];
+        slot_hist_add(hs, rec[q]);
+        const bool next_coded = lane < 63 && ((wbal[j][q] >> (lane + 1)) & 1ull);
+        if (coded && !next_coded) {
+          const unsigned long long above = lane < 63 ? (wbal[j][q] >> (lane + 1)) : 0ull;
+          const int nx = above ? p + 1 + (int)__builtin_ctzll(above) : next_coded_local(mask[j], p | 63);
+          if (nx < ENC_TILE && nx > p + 1) {
+            uint32_t mm = (uint32_t)(nx - p - 2);
+            while (true) {
+              atomicAdd(&run_hist[mm & 7u], 1u);
+              if (mm < 8) break;
+              mm >>= 3;
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < N_BINS; k += CLS_THREADS) {
+    uint32_t v = slot_hist_bin(hs, k);
+    if (k >= BIN_PREFIX + P_RUN1 && k < BIN_PREFIX + P_RUN1 + 8) v += run_hist[k - BIN_PREFIX - P_RUN1];
+    if (v) atomicAdd(&a.hist[(uint64_t)f * N_BINS + k], v);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // K2: runs crossing tile ends. One block (1024 threads) per frame.
