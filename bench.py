@@ -190,8 +190,8 @@ def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
 def config4_one_gpu(torch, nice, device, side, reps=3):
     """BASELINE config 4 on one GPU: the side x side RGBA image (SYN-v1 seed 11)
     encoded whole (one-frame batch) and through the band C ABI in 8 bands in
-    this process (the 8-rank split, exchanges on the host); both streams must
-    be identical."""
+    this process (the 8-rank split, each band on its own HIP stream, exchanges
+    as device tensor ops with one host read); both streams must be identical."""
     S = importlib.import_module(PKG + ".sharded")
     W = H = side
     img = syn_frames(torch, 1, W, H, 11, device)
@@ -207,12 +207,12 @@ def config4_one_gpu(torch, nice, device, side, reps=3):
     torch.cuda.synchronize()
     t_whole = (time.perf_counter() - t0) / reps
     flat = img.view(-1)
-    bes = []
-    band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes)   # warmup (contexts, scratch)
+    bes, sts = [], []
+    band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes, sts)   # warmup (contexts, scratch)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes)
+        band = S.encode_bands(flat, W, H, 4, 8, device.index or 0, bes, sts)
     torch.cuda.synchronize()
     t_band = (time.perf_counter() - t0) / reps
     n = int(ln[0])

@@ -47,6 +47,7 @@ EXPORTS = [
     "nice_decode", "nice_ctx_create", "nice_ctx_destroy", "nice_ctx_reserve",
     "nice_encode_batch_dev", "nice_decode_batch_dev",
     "nice_band_classify", "nice_band_runs", "nice_band_tables", "nice_band_words", "nice_band_pack",
+    "nice_band_runs_dev", "nice_band_tables_dev", "nice_band_pack_bits",
     "nice_band_assemble", "nice_tile_pixels",
     "nice_pipe_create", "nice_pipe_destroy", "nice_pipe_stream_stride", "nice_pipe_encode",
     "nice_pipe_decode",

@@ -55,7 +55,7 @@ struct EncLayout {
   size_t zero_bytes, total;
   size_t o_hist, o_flags, o_ctr, o_status;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc, o_bhist;
 };
 
 EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
@@ -85,6 +85,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   L.o_dend = take((size_t)n_frames * 8);
   L.o_packtab = take((size_t)n_frames * sizeof(PackTab));
   L.o_gacc = take((size_t)n_frames * ((T + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES + 1) * 8);
+  L.o_bhist = take((size_t)N_BINS * 4);   // band API: the band's own histogram
   L.total = o;
   return L;
 }
@@ -143,6 +144,7 @@ struct BandState {
   bool classified = false, tabled = false;
   nice::EncArgs a{};
   uint64_t band_bits = 0, seed_bit = 0;
+  uint32_t* bhist = nullptr;   // the band's own symbol counts (nice_band_runs), for its bit count
 };
 
 struct nice_ctx {
@@ -776,8 +778,10 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   a.px_lo = (int64_t)px0;
   a.px_hi = (int64_t)(px0 + px_count);
   a.band = 1;
-  a.pack_mode = 1;   // tile offsets from enc_tilescan (the band's bit offset comes from the exchange)
-  a.long_only = 0;
+  // one-pass packer with look-back from band_bit0; FLAG_LONG bands take the
+  // long-code path (tile bits, their scan) like frames
+  a.pack_mode = 0;
+  a.long_only = 1;
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
   const uint64_t work = tile_hi - tile_lo;
   uint64_t blocks = 2048, per = (work + blocks - 1) / blocks;
@@ -797,19 +801,50 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   NICE_HIP(hipGetLastError());
   ctx->bs = BandState{};
   ctx->bs.a = a;
+  ctx->bs.bhist = (uint32_t*)(base + L.o_bhist);
   ctx->bs.classified = true;
   return NICE_OK;
 }
 
-int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_hist) {
+static int band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, const uint32_t* d_band_next,
+                     uint32_t* d_hist) {
   if (!ctx || !d_hist || !ctx->bs.classified) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   EncArgs& a = ctx->bs.a;
   a.band_next = band_next;
+  a.band_next_dev = d_band_next;
   if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, 1), dim3(256), 0, st, a, 0);
   hipLaunchKernelGGL(enc_tailruns, dim3(a.groups, 1), dim3(1024), 0, st, a);
+  a.band_next_dev = nullptr;
+  NICE_HIP(hipMemcpyAsync(ctx->bs.bhist, a.hist, N_BINS * 4, hipMemcpyDeviceToDevice, st));
   NICE_HIP(hipMemcpyAsync(d_hist, a.hist, N_BINS * 4, hipMemcpyDeviceToDevice, st));
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+
+int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_hist) {
+  return band_runs(ctx, stream, band_next, nullptr, d_hist);
+}
+
+int nice_band_runs_dev(nice_ctx* ctx, void* stream, const uint32_t* d_band_next, uint32_t* d_hist) {
+  if (!d_band_next) return NICE_E_ARG;
+  return band_runs(ctx, stream, 0, d_band_next, d_hist);
+}
+
+// Code tables from the summed histogram, the header into the context's header
+// buffer, the band's bit count and the data start into d_info (device).
+static int band_tables(nice_ctx* ctx, hipStream_t st, const uint32_t* d_hist_total, unsigned long long* d_info) {
+  EncArgs& a = ctx->bs.a;
+  NICE_HIP(hipMemcpyAsync(a.hist, d_hist_total, N_BINS * 4, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(enc_tables, dim3(N_STREAMS), dim3(64), 0, st, a);
+  EncArgs h = a;   // the header goes to the context's header buffer
+  h.out = (uint8_t*)ctx->band_hdr.ptr;
+  h.out_stride = 4096;
+  h.out_len = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
+  hipLaunchKernelGGL(enc_header, dim3(1), dim3(64), 0, st, h);
+  hipLaunchKernelGGL(enc_packtab, dim3(1), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_band_sum, dim3(1), dim3(256), 0, st, a, (const uint32_t*)ctx->bs.bhist, d_info);
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }
@@ -819,20 +854,10 @@ int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, 
   if (!ctx || !d_hist_total || !ctx->bs.classified) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
-  EncArgs& a = ctx->bs.a;
-  int rc = ctx->band_hdr.grow(4096 + 16);
+  int rc = ctx->band_hdr.grow(4096 + 64);
   if (rc) return rc;
-  NICE_HIP(hipMemcpyAsync(a.hist, d_hist_total, N_BINS * 4, hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(enc_tables, dim3(N_STREAMS), dim3(64), 0, st, a);
-  EncArgs h = a;   // the header goes to the context's header buffer
-  h.out = (uint8_t*)ctx->band_hdr.ptr;
-  h.out_stride = 4096;
-  h.out_len = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
-  hipLaunchKernelGGL(enc_header, dim3(1), dim3(64), 0, st, h);
-  hipLaunchKernelGGL(enc_packtab, dim3(1), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(enc_tilebits, dim3(std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u)), dim3(256), 0, st, a);
-  unsigned long long* info = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096);
-  hipLaunchKernelGGL(enc_band_sum, dim3(1), dim3(256), 0, st, a, info);
+  unsigned long long* info = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096 + 16);
+  if ((rc = band_tables(ctx, st, d_hist_total, info))) return rc;
   unsigned long long hinfo[2];
   NICE_HIP(hipMemcpyAsync(hinfo, info, 16, hipMemcpyDeviceToHost, st));
   NICE_HIP(hipStreamSynchronize(st));
@@ -844,16 +869,37 @@ int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, 
   return NICE_OK;
 }
 
+int nice_band_tables_dev(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, uint64_t* d_info) {
+  if (!ctx || !d_hist_total || !d_info || !ctx->bs.classified) return NICE_E_ARG;
+  NICE_HIP(hipSetDevice(ctx->device));
+  int rc = ctx->band_hdr.grow(4096 + 64);
+  if (rc) return rc;
+  if ((rc = band_tables(ctx, (hipStream_t)stream, d_hist_total, (unsigned long long*)d_info))) return rc;
+  ctx->bs.tabled = true;
+  ctx->bs.band_bits = ~0ull;   // known to the caller once d_info is read (nice_band_pack_bits)
+  ctx->bs.seed_bit = ~0ull;
+  return NICE_OK;
+}
+
 uint32_t nice_tile_pixels(void) { return ENC_TILE; }
 
-uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits) {
+// the stream words the band touches, then a two-word trailer (a deferred
+// wrapped write, enc_band_fix)
+static uint64_t band_data_words(uint64_t band_bit0, uint64_t band_bits) {
   return band_bits ? ((band_bit0 + band_bits + 31) >> 5) - (band_bit0 >> 5) : 0;
 }
 
-int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_words, uint64_t words_cap) {
+uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits) {
+  return band_bits ? band_data_words(band_bit0, band_bits) + 2 : 0;
+}
+
+int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_t band_bits, uint32_t* d_words,
+                        uint64_t words_cap) {
   if (!ctx || !ctx->bs.tabled) return NICE_E_ARG;
-  const uint64_t nw = nice_band_words(band_bit0, ctx->bs.band_bits);
-  if (nw > words_cap || (nw && !d_words) || band_bit0 < ctx->bs.seed_bit) return NICE_E_ARG;
+  const uint64_t nw = nice_band_words(band_bit0, band_bits);
+  if (nw > words_cap || (nw && !d_words)) return NICE_E_ARG;
+  if (ctx->bs.seed_bit != ~0ull && band_bit0 < ctx->bs.seed_bit) return NICE_E_ARG;
+  ctx->bs.band_bits = band_bits;
   if (nw == 0) return NICE_OK;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
@@ -861,16 +907,33 @@ int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_
   a.band_bit0 = band_bit0;
   a.out = (uint8_t*)d_words - (int64_t)(band_bit0 >> 5) * 4;   // virtual: stream word w at d_words[w - w0]
   a.out_stride = 0;
-  const uint32_t tblocks = std::min<uint32_t>(a.tile_hi - a.tile_lo, 2048u);
+  a.band_fix = d_words + (nw - 2);
+  NICE_HIP(hipMemsetAsync(a.band_fix, 0, 8, st));
+  // the first word holds the previous band's last bits: only OR-ed into (enc_edges)
+  NICE_HIP(hipMemsetAsync(d_words, 0, 4, st));
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;
+  NICE_HIP(hipMemsetAsync(a.status, 0, (size_t)ng * 8, st));
+  NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
+  // FLAG_LONG (the launches return at once otherwise): tile bits, their scan from
+  // band_bit0, the codes that fit the cache, then the wrapped writes
+  const uint32_t tblocks = std::min<uint32_t>(nt, 2048u);
+  hipLaunchKernelGGL(enc_tilebits, dim3(tblocks), dim3(256), 0, st, a);
   if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, 1), dim3(256), 0, st, a, 1);
   hipLaunchKernelGGL(enc_tilescan, dim3(a.groups, 1), dim3(1024), 0, st, a);
-  NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
-  hipLaunchKernelGGL(enc_pack, dim3((uint32_t)std::min<uint64_t>(a.tile_hi - a.tile_lo, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU)),
-                     dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 0);
   hipLaunchKernelGGL(enc_pack_long, dim3(tblocks), dim3(256), 0, st, a, 1);
+  // every other band: one pass, group offsets by look-back from band_bit0
+  hipLaunchKernelGGL(enc_pack, dim3((uint32_t)std::min<uint64_t>(nt, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU)),
+                     dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_edges, dim3(std::min<uint32_t>((ng + 255) / 256, 64u), 1), dim3(256), 0, st, a);
   NICE_HIP(hipGetLastError());
   return NICE_OK;
+}
+
+int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_words, uint64_t words_cap) {
+  if (!ctx || !ctx->bs.tabled || ctx->bs.band_bits == ~0ull) return NICE_E_ARG;
+  return nice_band_pack_bits(ctx, stream, band_bit0, ctx->bs.band_bits, d_words, words_cap);
 }
 
 int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, const uint64_t* band_bit0,
@@ -878,17 +941,21 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
                        uint64_t* out_len) {
   if (!ctx || !ctx->bs.tabled || !d_out || !out_len || n_bands == 0 || !band_bit0 || !band_bits)
     return NICE_E_ARG;
-  const uint64_t seed = ctx->bs.seed_bit;
-  std::vector<unsigned long long> meta(2 * n_bands + 1);
+  // the data start: learned by nice_band_tables, else the first band's start
+  const uint64_t seed = ctx->bs.seed_bit != ~0ull ? ctx->bs.seed_bit : band_bit0[0];
+  // meta: band first words [R], band offsets [R + 1], data end, out_len, band first bits [R]
+  std::vector<unsigned long long> meta(3 * n_bands + 3);
   uint64_t off = 0, end = seed;
   for (uint32_t r = 0; r < n_bands; ++r) {
     if (band_bit0[r] != end) return NICE_E_ARG;   // bands must tile the data bits
     meta[r] = band_bit0[r] >> 5;
     meta[n_bands + r] = off;
+    meta[2 * n_bands + 3 + r] = band_bit0[r];
     off += nice_band_words(band_bit0[r], band_bits[r]);
     end += band_bits[r];
   }
   meta[2 * n_bands] = off;
+  meta[2 * n_bands + 1] = end;
   const uint64_t B = end >> 3;
   if (B + 5 > out_cap || (((uintptr_t)d_out) & 3)) return NICE_E_CAPACITY;
   NICE_HIP(hipSetDevice(ctx->device));
@@ -903,18 +970,22 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
   const uint64_t hdr_words = (seed + 31) >> 5, end_words = (end + 31) >> 5;
   if (end_words > hdr_words)
     NICE_HIP(hipMemsetAsync(d_out + hdr_words * 4, 0, (end_words - hdr_words) * 4, st));
-  if (off)
-    hipLaunchKernelGGL(enc_band_merge, dim3(64, n_bands), dim3(256), 0, st, (uint32_t*)d_out, d_words, dmeta,
+  if (off) {
+    uint64_t most = 0;
+    for (uint32_t r = 0; r < n_bands; ++r) most = std::max<uint64_t>(most, meta[n_bands + r + 1] - meta[n_bands + r]);
+    hipLaunchKernelGGL(enc_band_merge, dim3((uint32_t)((most + 4095) / 4096), n_bands), dim3(256), 0, st,
+                       (uint32_t*)d_out, d_words, dmeta, dmeta + n_bands, n_bands);
+    hipLaunchKernelGGL(enc_band_fix, dim3(1), dim3(64), 0, st, d_out, d_words, dmeta + 2 * n_bands + 3,
                        dmeta + n_bands, n_bands);
+  }
   EncArgs a = ctx->bs.a;
   a.out = d_out;
   a.out_stride = 0;
   a.n_frames = 1;
   a.data_end = dmeta + 2 * n_bands + 1;
   a.out_len = dmeta + 2 * n_bands + 2;
-  NICE_HIP(hipMemcpyAsync(a.data_end, &end, 8, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(enc_tail, dim3(1), dim3(64), 0, st, a);
-  NICE_HIP(hipStreamSynchronize(st));   // `end` lives on this stack frame
+  NICE_HIP(hipStreamSynchronize(st));   // `meta` lives on this stack frame
   *out_len = B + 5;
   NICE_HIP(hipGetLastError());
   return NICE_OK;

@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
   const uint32_t N = a.W * a.H;
   // the first coded pixel after the group: later groups, then after the band
   // (frames: none)
-  uint32_t after = a.band ? (uint32_t)a.band_next : NONE;
+  uint32_t after = a.band ? (a.band_next_dev ? *a.band_next_dev : (uint32_t)a.band_next) : NONE;
   for (uint32_t k = g + 1; k < a.groups; ++k) after = min(after, (uint32_t)a.gacc[(uint64_t)f * a.groups + k]);
   const uint32_t per = (nt + TR_THREADS - 1) / TR_THREADS;
   const uint32_t c0 = threadIdx.x * per;
@@ -1442,7 +1442,6 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
 // A thread owns 4 consecutive pixels and reads their records with one 16-byte
 // load.
 // ---------------------------------------------------------------------------
-constexpr int PACK_SUB = 4;                                // tiles per enc_pack work item
 constexpr int PACK_CAP_BITS = PACK_SUB * ENC_TILE * 32;    // LDS bit buffer: <= 32 bits per pixel
 constexpr int PACK_MAX_WORDS = PACK_CAP_BITS / 32 + 2;
 constexpr int PK_THREADS = 256;
@@ -1963,7 +1962,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
       __syncthreads();   // wsum and mask are rewritten by the next tile
     }
     if (wid == 0 && lookback_mode) {
-      const unsigned long long off = lookback(a.status, f * ng + g, g, a.seed_bit[f], gbits, lane);
+      const unsigned long long off = lookback(a.status, f * ng + g, g, a.band ? a.band_bit0 : a.seed_bit[f], gbits, lane);
       if (lane == 0) s_off = off;
     }
     __syncthreads();
@@ -2076,12 +2075,12 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
 // into that word once every group has stored its own words.
 __global__ __launch_bounds__(256) void enc_edges(EncArgs a) {
   const uint32_t T = a.tiles_per_frame;
-  const uint32_t ng = (T + PACK_SUB - 1) / PACK_SUB;
+  const uint32_t ng = (a.tile_hi - a.tile_lo + PACK_SUB - 1) / PACK_SUB;   // groups of the frame (band)
   for (uint32_t f = blockIdx.y; f < a.n_frames; f += gridDim.y) {
     if (a.frame_flags[f] & FLAG_LONG) continue;
     uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
     for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < ng; g += gridDim.x * 256) {
-      const uint64_t t = (uint64_t)f * T + (uint64_t)g * PACK_SUB;
+      const uint64_t t = (uint64_t)f * T + a.tile_lo + (uint64_t)g * PACK_SUB;
       const uint32_t e = a.tile_bits[t];
       if (e) atomicOr(&out32[a.tile_off[t] >> 5], __builtin_bswap32(e));
     }
@@ -2122,9 +2121,11 @@ __global__ __launch_bounds__(64) void enc_tail(EncArgs a) {
 // Phase 1 re-derives every symbol's position and applies the wrapped writes to
 // their windows, whose earlier bits phase 0 has finalised.  Wrapped windows
 // are disjoint: a window ends before its code's end (p + n > window + 32),
-// and the next code starts there.  In band mode a window never reaches into
-// the previous band: a band's first code is the prefix code of its first coded
-// pixel (stream SC_PREFIXES, 13 symbols: at most 12 bits), never a long one.
+// and the next code starts there.  In band mode a window that starts in the
+// byte holding band_bit0 also covers (and may carry into) the previous band's
+// last bits: at most one per band (n >= 26), so it is recorded in the band's
+// two trailer words (band_fix) and applied by enc_band_fix after the bands are
+// merged.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void wrapped_write(uint8_t* out, uint64_t p, uint32_t v, uint32_t n) {
   const uint64_t B = p >> 3;
@@ -2205,8 +2206,13 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
           atomicOr(&out32[pos >> 5], __builtin_bswap32((uint32_t)(y >> 32)));
           if (o + n > 32u) atomicOr(&out32[(pos >> 5) + 1], __builtin_bswap32((uint32_t)y));
         }
-      } else if (phase == 1 && !(a.band && (pos & ~7ull) < a.band_bit0)) {
-        wrapped_write(out, pos, v, n);
+      } else if (phase == 1) {
+        if (a.band && (pos & ~7ull) < a.band_bit0) {   // window reaches the previous band: deferred
+          a.band_fix[0] = 0x80000000u | ((uint32_t)(pos - a.band_bit0) << 8) | n;
+          a.band_fix[1] = v;
+        } else {
+          wrapped_write(out, pos, v, n);
+        }
       }
       pos += n;
     };
@@ -2245,12 +2251,38 @@ __global__ __launch_bounds__(256) void enc_band_merge(uint32_t* out32, const uin
   const uint32_t r = blockIdx.y;
   if (r >= R) return;
   const unsigned long long n = band_off[r + 1] - band_off[r];
+  if (n < 3) return;
+  const unsigned long long nd = n - 2;   // the last two words of a band are its trailer (enc_band_fix)
   const unsigned long long w0 = band_w0[r];
-  for (unsigned long long m = (unsigned long long)blockIdx.x * 256 + threadIdx.x; m < n;
-       m += (unsigned long long)gridDim.x * 256) {
-    const uint32_t v = words[band_off[r] + m];
-    if (m == 0 || m + 1 == n) atomicOr(&out32[w0 + m], v);   // shared with a neighbour or the header
-    else out32[w0 + m] = v;
+  const uint32_t* src = words + band_off[r];
+  // 16 words per thread in flight: block b covers words [4096 b, 4096 (b + 1))
+  constexpr int K = 16;
+  const unsigned long long m0 = (unsigned long long)blockIdx.x * (256 * K) + threadIdx.x;
+  if (m0 >= nd) return;
+  uint32_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long m = m0 + 256ull * k;
+    v[k] = m < nd ? src[m] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long m = m0 + 256ull * k;
+    if (m >= nd) break;
+    if (m == 0 || m + 1 == nd) atomicOr(&out32[w0 + m], v[k]);   // shared with a neighbour or the header
+    else out32[w0 + m] = v[k];
+  }
+}
+
+// The deferred wrapped writes, band by band (their windows are disjoint; each
+// reads the merged bits of the band before it).  One thread: at most R writes.
+__global__ void enc_band_fix(uint8_t* out, const uint32_t* words, const unsigned long long* band_bit0,
+                             const unsigned long long* band_off, uint32_t R) {
+  if (threadIdx.x != 0) return;
+  for (uint32_t r = 0; r < R; ++r) {
+    if (band_off[r + 1] == band_off[r]) continue;   // empty band: no trailer
+    const uint32_t f = words[band_off[r + 1] - 2];
+    if (f & 0x80000000u) wrapped_write(out, band_bit0[r] + ((f >> 8) & 0xFFu), words[band_off[r + 1] - 1], f & 0xFFu);
   }
 }
 
@@ -2279,16 +2311,34 @@ __global__ __launch_bounds__(256) void enc_band_edges(EncArgs a, uint32_t* edges
   }
 }
 
-__global__ __launch_bounds__(256) void enc_band_sum(EncArgs a, unsigned long long* info) {
-  __shared__ unsigned long long s;
-  if (threadIdx.x == 0) s = 0;
+// The band's data bits: its own symbol counts (bhist, 858 bins; the mode
+// prefixes derived from the payload streams as enc_tables does) times the code
+// lengths of the shared tables.  info = {bits, data start bit}.
+__global__ __launch_bounds__(256) void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info) {
+  __shared__ unsigned long long s_bits;
+  __shared__ uint32_t s_mode[5];
+  if (threadIdx.x == 0) s_bits = 0;
+  if (threadIdx.x < 5) s_mode[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long v = 0;
-  for (uint32_t t = a.tile_lo + threadIdx.x; t < a.tile_hi; t += 256) v += a.tile_bits[t];
-  atomicAdd(&s, v);
+  uint32_t c[5] = {0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < N_BINS; b += 256) {
+    const uint32_t h = bhist[b];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) c[k] += mode_id_bin(k, b) ? h : 0u;
+    if (b >= BIN_PREFIX && b < BIN_PREFIX + 5) continue;   // mode prefixes: below
+    v += (unsigned long long)h * a.tbl_len8[b];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (c[k]) atomicAdd(&s_mode[k], c[k]);
+  atomicAdd(&s_bits, v);
   __syncthreads();
   if (threadIdx.x == 0) {
-    info[0] = s;
+    unsigned long long bits = s_bits;
+    for (int k = 0; k < 5; ++k)
+      bits += (unsigned long long)(s_mode[k] / mode_id_syms(k)) * a.tbl_len8[BIN_PREFIX + k];
+    info[0] = bits;
     info[1] = a.seed_bit[0];
   }
 }

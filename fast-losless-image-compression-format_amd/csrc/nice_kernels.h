@@ -59,6 +59,8 @@ struct EncArgs {
   int64_t px_lo, px_hi;
   uint32_t band;
   unsigned long long band_next, band_bit0;
+  const uint32_t* band_next_dev;   // non-null: band_next read from device memory (nice_band_runs_dev)
+  uint32_t* band_fix;        // band pack: {flag | offset << 8 | length, code} of a wrapped write before band_bit0
   // the per-frame tile scans (enc_tailruns, enc_tilescan) run as `groups`
   // blocks of ENC_GROUP_TILES tiles per frame; gacc holds each group's
   // aggregate (n_frames * groups: min first coded pixel, then bit total)
@@ -91,9 +93,12 @@ __global__ void enc_packtab(EncArgs a);
 __global__ void enc_pack(EncArgs a);
 __global__ void enc_edges(EncArgs a);
 constexpr uint32_t PACK_BLOCKS_PER_CU = 4;   // enc_pack: 256 threads, ~35 KB LDS
+constexpr int PACK_SUB = 4;                  // tiles per enc_pack work item (group)
 __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
-__global__ void enc_band_sum(EncArgs a, unsigned long long* info);
+__global__ void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info);
+__global__ void enc_band_fix(uint8_t* out, const uint32_t* words, const unsigned long long* band_bit0,
+                             const unsigned long long* band_off, uint32_t R);
 __global__ void enc_band_merge(uint32_t* out32, const uint32_t* words, const unsigned long long* band_w0,
                                const unsigned long long* band_off, uint32_t R);
 // long-code frames (FLAG_LONG): phase 0 packs every code whose write does not

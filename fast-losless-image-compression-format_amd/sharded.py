@@ -17,9 +17,17 @@ the CPU tests):
    peers' transfers run concurrently over their own xGMI links), which ORs the
    shared boundary words and writes header and tail.
 
-A band step that fails on one rank (a NiceError from the C ABI) is reported
-through the next exchange (an error word rides along in each gathered or
-reduced tensor), so every rank raises instead of waiting in a collective.
+Steps 1-3 stay on the device: the next band's first coded pixel is reduced
+on the GPU and read by ``nice_band_runs_dev``, the summed histogram goes
+straight to ``nice_band_tables_dev``, whose bit count is gathered as a device
+tensor.  The host reads once, after step 3 (the word counts of step 4 size
+its buffers).
+
+A band step that fails on one rank (a NiceError from the C ABI, raised before
+anything is queued) is carried as an error word through every later exchange;
+the rank keeps taking part with empty results, so every rank raises together
+after step 3 (or, for the pack, after step 4) instead of waiting in a
+collective.
 
 The root's bytes equal ``encode_bytes`` of the whole image.  The band steps
 go through a *backend* object (``HipBands`` drives libnice_hip.so); the
@@ -54,7 +62,8 @@ def band_pixels(width: int, height: int, lo: int, hi: int, tile: int = 1024):
 
 
 class HipBands:
-    """Band steps on the GPU through the C ABI (include/nice.h)."""
+    """Band steps on the GPU through the C ABI (include/nice.h).  Results stay
+    on the device; nothing here waits for the GPU."""
 
     def __init__(self, device: int = 0):
         from . import _ctx, lib
@@ -64,11 +73,11 @@ class HipBands:
         L = self.L
         vp, u8, u32, u64 = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64
         L.nice_band_classify.argtypes = [vp, vp, vp, u64, u64, u32, u32, u8, u8, u32, u32, vp]
-        L.nice_band_runs.argtypes = [vp, vp, u32, vp]
-        L.nice_band_tables.argtypes = [vp, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.nice_band_runs_dev.argtypes = [vp, vp, vp, vp]
+        L.nice_band_tables_dev.argtypes = [vp, vp, vp, vp]
         L.nice_band_words.argtypes = [u64, u64]
         L.nice_band_words.restype = u64
-        L.nice_band_pack.argtypes = [vp, vp, u64, vp, u64]
+        L.nice_band_pack_bits.argtypes = [vp, vp, u64, u64, vp, u64]
         L.nice_band_assemble.argtypes = [vp, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), u32, vp, u64,
                                          ctypes.POINTER(u64)]
 
@@ -81,7 +90,11 @@ class HipBands:
         if rc != 0:
             raise NiceError(rc, what)
 
+    def _dev(self):
+        return f"cuda:{self.device}"
+
     def classify(self, px, px0, width, height, channels, channels_out, lo, hi):
+        """{first, last} coded pixel of the band (int64 device tensor, NONE: none)."""
         import torch
         edges = torch.empty(2, dtype=torch.int32, device=px.device)
         self._check(self.L.nice_band_classify(self.ctx.ptr, self._st(), ctypes.c_void_p(px.data_ptr()), px0,
@@ -90,30 +103,40 @@ class HipBands:
         return edges.to(torch.int64) & NONE
 
     def runs(self, band_next):
+        """The band's histogram (858 x int32, device); ``band_next``: a 0-d
+        integer tensor (any device) or an int."""
         import torch
-        hist = torch.empty(858, dtype=torch.int32, device=f"cuda:{self.device}")
-        self._check(self.L.nice_band_runs(self.ctx.ptr, self._st(), band_next, ctypes.c_void_p(hist.data_ptr())),
-                    "nice_band_runs")
+        bn = torch.as_tensor(band_next).reshape(1).to(device=self._dev(), dtype=torch.int32)
+        hist = torch.empty(858, dtype=torch.int32, device=self._dev())
+        self._bn = bn   # kept alive until the kernel has read it (stream order)
+        self._check(self.L.nice_band_runs_dev(self.ctx.ptr, self._st(), ctypes.c_void_p(bn.data_ptr()),
+                                              ctypes.c_void_p(hist.data_ptr())), "nice_band_runs_dev")
         return hist
 
     def tables(self, hist_total):
+        """Builds the tables; returns {band bits, data start bit} as an int64
+        device tensor."""
         import torch
-        bits, seed = ctypes.c_uint64(), ctypes.c_uint64()
         # the C ABI reads the histogram on this rank's GPU (gloo reduces on the host)
-        h = hist_total.to(device=f"cuda:{self.device}", dtype=torch.int32).contiguous()
-        self._check(self.L.nice_band_tables(self.ctx.ptr, self._st(), ctypes.c_void_p(h.data_ptr()),
-                                            ctypes.byref(bits), ctypes.byref(seed)), "nice_band_tables")
-        return int(bits.value), int(seed.value)
+        h = hist_total.to(device=self._dev(), dtype=torch.int32).contiguous()
+        info = torch.empty(2, dtype=torch.int64, device=self._dev())
+        self._h = h
+        self._check(self.L.nice_band_tables_dev(self.ctx.ptr, self._st(), ctypes.c_void_p(h.data_ptr()),
+                                                ctypes.c_void_p(info.data_ptr())), "nice_band_tables_dev")
+        return info
 
     def words(self, bit0, bits):
         return int(self.L.nice_band_words(bit0, bits))
 
-    def pack(self, bit0, bits):
+    def pack(self, bit0, bits, out=None):
+        """The band's words (``words(bit0, bits)`` int32, device); into ``out``
+        when given."""
         import torch
         n = self.words(bit0, bits)
-        out = torch.zeros(max(n, 1), dtype=torch.int32, device=f"cuda:{self.device}")
-        self._check(self.L.nice_band_pack(self.ctx.ptr, self._st(), bit0, ctypes.c_void_p(out.data_ptr()), n),
-                    "nice_band_pack")
+        if out is None:
+            out = torch.empty(max(n, 1), dtype=torch.int32, device=self._dev())
+        self._check(self.L.nice_band_pack_bits(self.ctx.ptr, self._st(), bit0, bits,
+                                               ctypes.c_void_p(out.data_ptr()), n), "nice_band_pack_bits")
         return out[:n]
 
     def assemble(self, words_cat, bit0s, bitss, width, height):
@@ -121,7 +144,7 @@ class HipBands:
         from . import encode_bound
         R = len(bit0s)
         cap = encode_bound(width, height)
-        out = torch.empty((cap + 3) // 4 * 4, dtype=torch.uint8, device=f"cuda:{self.device}")
+        out = torch.empty((cap + 3) // 4 * 4, dtype=torch.uint8, device=self._dev())
         b0 = (ctypes.c_uint64 * R)(*bit0s)
         bb = (ctypes.c_uint64 * R)(*bitss)
         n = ctypes.c_uint64()
@@ -147,6 +170,19 @@ def _raise_if(err: int, what: str):
         raise NiceError(err, what + " (on some rank)")
 
 
+STEPS = ("nice_band_classify", "nice_band_runs", "nice_band_tables", "nice_band_pack")
+
+
+def band_next_of(firsts, n: int):
+    """For each band, the first coded pixel of the bands after it (``n``: none):
+    a suffix minimum over the bands' first coded pixels (int64 tensor, NONE
+    for a band without one), on the tensor's device."""
+    import torch
+    f = torch.where(firsts == NONE, torch.full_like(firsts, n), firsts)
+    nxt = torch.cat([f[1:], f.new_full((1,), n)])
+    return torch.flip(torch.cummin(torch.flip(nxt, [0]), 0).values, [0])
+
+
 def encode_sharded(backend, dist, px, px0: int, width: int, height: int, channels: int,
                    channels_out: int | None = None, root: int = 0, device=None):
     """Encode one image across the ranks of the default process group.
@@ -161,89 +197,148 @@ def encode_sharded(backend, dist, px, px0: int, width: int, height: int, channel
     co = channels if channels_out is None else channels_out
     n = width * height
     lo, hi = band_tiles(width, height, rank, world)
-    # 1. edges -> the first coded pixel after this band (+ error word)
-    edges, err = _step(backend.classify, px, px0, width, height, channels, co, lo, hi)
+    err, err_step = 0, 0
+
+    def note(e, k):
+        nonlocal err, err_step
+        if e and not err:
+            err, err_step = e, k
+
+    # 1. edges -> the first coded pixel after this band, reduced on the device
+    edges, e = _step(backend.classify, px, px0, width, height, channels, co, lo, hi)
+    note(e, 0)
     if edges is None:
         edges = torch.full((2,), NONE, dtype=torch.int64)
-    mine = torch.cat([edges.to(device=dev, dtype=torch.int64),
-                      torch.tensor([err], dtype=torch.int64, device=dev)])
+    mine = edges.to(device=dev, dtype=torch.int64)
     all_edges = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(all_edges, mine)
-    ge = torch.stack(all_edges).cpu()
-    _raise_if(int(ge[:, 2].min()), "nice_band_classify")
-    later = [int(e[0]) for e in ge[rank + 1:] if int(e[0]) != NONE]
-    band_next = later[0] if later else n
-    # 2. histogram -> identical tables everywhere (error count in the last slot)
-    hist, err = _step(backend.runs, band_next)
-    h = torch.zeros(859, dtype=torch.int64, device=dev)
+    band_next = band_next_of(torch.stack(all_edges)[:, 0], n)[rank]
+    # 2. histogram -> identical tables everywhere
+    hist, e = _step(backend.runs, band_next)
+    note(e, 1)
+    h = torch.zeros(858, dtype=torch.int64, device=dev)
     if hist is not None:
-        h[:858] = hist.to(device=dev, dtype=torch.int64)
-    h[858] = 1 if err else 0
+        h += hist.to(device=dev, dtype=torch.int64)
     dist.all_reduce(h)
-    _raise_if(-1 if int(h[858]) else 0, "nice_band_runs")
-    res, err = _step(backend.tables, h[:858])
-    bits, seed = res if res is not None else (0, 0)
-    # 3. bit counts -> offsets
-    b = torch.tensor([bits, err], dtype=torch.int64, device=dev)
+    info, e = _step(backend.tables, h)
+    note(e, 2)
+    # 3. bit counts -> offsets (+ every rank's error word): the one host read
+    b = torch.zeros(4, dtype=torch.int64, device=dev)
+    if info is not None:
+        b[:2] = info.to(device=dev, dtype=torch.int64)
+    b[2:] = torch.tensor([err, err_step], dtype=torch.int64).to(dev)
     all_bits = [torch.empty_like(b) for _ in range(world)]
     dist.all_gather(all_bits, b)
     gb = torch.stack(all_bits).cpu()
-    _raise_if(int(gb[:, 1].min()), "nice_band_tables")
+    bad = [r for r in range(world) if int(gb[r, 2])]
+    if bad:
+        _raise_if(int(gb[bad[0], 2]), STEPS[int(gb[bad[0], 3])])
     bitss = [int(x) for x in gb[:, 0]]
+    seed = int(gb[0, 1])
     bit0s = [seed + sum(bitss[:r]) for r in range(world)]
-    words = backend.pack(bit0s[rank], bitss[rank])
-    # 4. gather-v of the band words to the root: grouped P2P, all peers at once
+    words, e = _step(backend.pack, bit0s[rank], bitss[rank])
+    # 4. gather-v of the band words to the root: grouped P2P, all peers at once;
+    # a rank whose pack failed sends zeros of the agreed size, then the error
+    # words are reduced so every rank raises together
     counts = [backend.words(bit0s[r], bitss[r]) for r in range(world)]
+    if words is None:
+        words = torch.zeros(counts[rank], dtype=torch.int32, device=dev)
     if rank != root:
         if counts[rank]:
             for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, words.to(dev).contiguous(), root)]):
                 q.wait()
+    else:
+        parts, ops = [], []
+        for r in range(world):
+            if r == rank:
+                parts.append(words.to(dev))
+            elif counts[r]:
+                buf = torch.empty(counts[r], dtype=words.dtype, device=dev)
+                ops.append(dist.P2POp(dist.irecv, buf, r))
+                parts.append(buf)
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+    pe = torch.tensor([e], dtype=torch.int64).to(dev)
+    dist.all_reduce(pe, op=dist.ReduceOp.MIN)   # NiceError codes are negative
+    _raise_if(int(pe), STEPS[3])
+    if rank != root:
         return None
-    parts, ops = [], []
-    for r in range(world):
-        if r == rank:
-            parts.append(words.to(dev))
-        elif counts[r]:
-            buf = torch.empty(counts[r], dtype=words.dtype, device=dev)
-            ops.append(dist.P2POp(dist.irecv, buf, r))
-            parts.append(buf)
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
     cat = torch.cat(parts) if parts else words.new_zeros(0)
     return backend.assemble(cat.to(words.device), bit0s, bitss, width, height)
 
 
 def encode_bands(px, width: int, height: int, channels: int, n_bands: int, device: int = 0,
-                 backends: list | None = None):
+                 backends: list | None = None, streams: list | None = None, ranges: list | None = None,
+                 stats: dict | None = None):
     """The band C ABI driven in ONE process: ``n_bands`` bands (the split
-    ``n_bands`` ranks would use), each with its own context, the exchange steps
-    done on the host.  ``px``: the whole image (uint8 cuda tensor).  Returns
-    the stream (uint8 cuda tensor), equal to encoding the image whole.
-    ``backends``: reuse contexts across calls (a list, filled on first use)."""
+    ``n_bands`` ranks would use), each with its own context and HIP stream so
+    the bands' kernels overlap on the GPU; the exchanges are device tensor ops
+    with one host read (the bit counts).  ``px``: the whole image (uint8 cuda
+    tensor).  Returns the stream (uint8 cuda tensor), equal to encoding the
+    image whole.  ``backends``/``streams``: reuse across calls (lists, filled
+    on first use).  ``ranges``: the bands' tile ranges (default: the even
+    split of ``band_tiles``).  ``stats``: if a dict, receives "bit0s", "bits"
+    and "deferred" (bands whose trailer holds a deferred wrapped write)."""
     import torch
     from . import _Ctx
     w, h, c, R = width, height, channels, n_bands
     N = w * h
     if backends is None:
         backends = []
+    if streams is None:
+        streams = []
     while len(backends) < R:
         be = HipBands(device)
         be.ctx = _Ctx(device)   # a context holds one band's state between the steps
         backends.append(be)
-    bands = backends[:R]
-    ranges = [band_tiles(w, h, r, R) for r in range(R)]
-    firsts = []
-    for be, (lo, hi) in zip(bands, ranges):
-        p0, p1 = band_pixels(w, h, lo, hi)
-        firsts.append(int(be.classify(px[p0 * c: p1 * c], p0, w, h, c, c, lo, hi)[0]))
-    hist = None
-    for r, be in enumerate(bands):
-        later = [f for f in firsts[r + 1:] if f != NONE]
-        hr = be.runs(later[0] if later else N)
-        hist = hr.clone() if hist is None else hist + hr
-    bits, seeds = zip(*[be.tables(hist) for be in bands])
-    assert len(set(seeds)) == 1
-    bit0s = [seeds[0] + sum(bits[:r]) for r in range(R)]
-    words = torch.cat([be.pack(bit0s[r], bits[r]) for r, be in enumerate(bands)])
-    return bands[0].assemble(words, bit0s, list(bits), w, h)
+    while len(streams) < R:
+        streams.append(torch.cuda.Stream(device))
+    bands, sts = backends[:R], streams[:R]
+    main = torch.cuda.current_stream(device)
+    if ranges is None:
+        ranges = [band_tiles(w, h, r, R) for r in range(R)]
+    assert len(ranges) == R
+    edges = []
+    for be, st, (lo, hi) in zip(bands, sts, ranges):
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            p0, p1 = band_pixels(w, h, lo, hi)
+            edges.append(be.classify(px[p0 * c: p1 * c], p0, w, h, c, c, lo, hi))
+    for st in sts:
+        main.wait_stream(st)
+    nxt = band_next_of(torch.stack(edges)[:, 0], N).to(torch.int32)
+    hists = []
+    for r, (be, st) in enumerate(zip(bands, sts)):
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            hists.append(be.runs(nxt[r]))
+    for st in sts:
+        main.wait_stream(st)
+    hist = torch.stack(hists).sum(0, dtype=torch.int32)
+    infos = []
+    for be, st in zip(bands, sts):
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            infos.append(be.tables(hist))
+    for st in sts:
+        main.wait_stream(st)
+    info = torch.stack(infos).cpu()   # the one host read
+    bits = [int(x) for x in info[:, 0]]
+    seed = int(info[0, 1])
+    bit0s = [seed + sum(bits[:r]) for r in range(R)]
+    counts = [bands[0].words(bit0s[r], bits[r]) for r in range(R)]
+    words = torch.empty(max(sum(counts), 1), dtype=torch.int32, device=px.device)
+    off = 0
+    for r, (be, st) in enumerate(zip(bands, sts)):
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            be.pack(bit0s[r], bits[r], words[off: off + counts[r]])
+        off += counts[r]
+    for st in sts:
+        main.wait_stream(st)
+    if stats is not None:
+        ends = [sum(counts[: r + 1]) for r in range(R)]
+        stats.update(bit0s=bit0s, bits=bits, deferred=[r for r in range(R) if counts[r] and
+                                                         int(words[ends[r] - 2]) & 0x80000000])
+    return bands[0].assemble(words[:off], bit0s, bits, w, h)

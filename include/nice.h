@@ -110,7 +110,18 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
  *                           stream position (first/last word partial)
  *   5. gather words         nice_band_assemble (one rank): header + bands + tail
  * The result equals nice_encode of the whole image byte for byte, codes longer
- * than 25 bits included.
+ * than 25 bits included.  nice_band_words() counts the band's stream words plus
+ * a two-word trailer: a code longer than 25 bits that starts in the byte
+ * holding band_bit0 rewrites (reference writer wrap, bitwriter.rs:55-73) bits
+ * of the previous band; it is recorded there and applied by nice_band_assemble.
+ * Device-resident variants (no host synchronisation between the steps; the
+ * exchanges can stay on device, e.g. RCCL collectives on the same stream):
+ *   nice_band_runs_dev      band_next read from device memory (u32)
+ *   nice_band_tables_dev    d_info[0] = the band's data bits, d_info[1] = the
+ *                           data start bit (device u64 x 2, written in stream order)
+ *   nice_band_pack_bits     the band's bits passed in (from the gathered d_info)
+ * nice_band_assemble after nice_band_tables_dev takes band_bit0[0] as the data
+ * start.
  * d_px holds pixels [px0, px0 + px_count) (global raster index), which must
  * cover the band and the 3 rows + 3 pixels before it. */
 int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_t px0, uint64_t px_count,
@@ -119,8 +130,12 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
 int nice_band_runs(nice_ctx* ctx, void* stream, uint32_t band_next, uint32_t* d_hist);
 int nice_band_tables(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, uint64_t* band_bits,
                      uint64_t* seed_bit);
+int nice_band_runs_dev(nice_ctx* ctx, void* stream, const uint32_t* d_band_next, uint32_t* d_hist);
+int nice_band_tables_dev(nice_ctx* ctx, void* stream, const uint32_t* d_hist_total, uint64_t* d_info);
 uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits);
 int nice_band_pack(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint32_t* d_words, uint64_t words_cap);
+int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_t band_bits, uint32_t* d_words,
+                        uint64_t words_cap);
 int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, const uint64_t* band_bit0,
                        const uint64_t* band_bits, uint32_t n_bands, uint8_t* d_out, uint64_t out_cap,
                        uint64_t* out_len);

@@ -975,13 +975,37 @@ void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C) {
  * small diffs drawn with weights F(k+2); a draw is rejected when it would
  * make the pixel a run member or a back reference (code.rs:191-206, 371-407)
  * or leave 0..255; pixels with no valid draw take a large jump (RGB / luma). */
-void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K) {
+/* Pixel i takes delta dl: in range, drifting toward mid-range, and coded
+ * (not a run member) with no back reference k = 1..4.  Writes p on success. */
+static int deep_try(uint8_t *px, size_t i, uint32_t W, uint32_t C, const int pred[3], const int dl[3]) {
+    uint8_t *p = px + i * C;
+    int v[3];
+    for (int c = 0; c < 3; ++c) {
+        v[c] = pred[c] + dl[c];
+        if (v[c] < 0 || v[c] > 255) return 0;
+        if ((pred[c] > 215 && dl[c] > 0) || (pred[c] < 40 && dl[c] < 0)) return 0;
+    }
+    for (int c = 0; c < 3; ++c) p[c] = (uint8_t)v[c];
+    const size_t q = i * C;
+    if (rgb_eq(px, q, q - C)) return 0;
+    if (i >= W && rgb_eq(px, q, q - (size_t)W * C)) return 0;
+    if (i >= W - 1 && W >= 1 && rgb_eq(px, q, q - (size_t)(W - 1) * C)) return 0;
+    if (i >= 2 && rgb_eq(px, q, q - 2 * (size_t)C)) return 0;
+    if (i >= 2 * (size_t)W && rgb_eq(px, q, q - 2 * (size_t)W * C)) return 0;
+    return 1;
+}
+
+/* force (ascending pixel indices): those pixels take the rarest delta still
+ * available, so the rarest (longest-code) symbols land there. */
+static void gen_deep(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
+                     const uint64_t *force, size_t n_force) {
     if (K > 40) K = 40;
     if (K < 2) K = 2;
     int dl[40][3];
     uint64_t left[40], total = 0;
     uint64_t fa = 1, fb = 2;   /* F(2), F(3) */
     uint32_t s = seed ? seed : 1u;
+    size_t fi = 0;
 #define XS() (s ^= s << 13, s ^= s >> 17, s ^= s << 5, s)
     for (uint32_t k = 0; k < K; ++k) {
         /* distinct nonzero deltas, alternating in sign by rank */
@@ -1003,26 +1027,15 @@ void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C,
         for (int c = 0; c < 3; ++c)
             pred[c] = i >= W ? ((int)px[(i - W) * C + c] + (int)L[c]) / 2 : (int)L[c];
         int ok = 0;
+        while (fi < n_force && force[fi] < i) ++fi;
+        if (fi < n_force && force[fi] == i)
+            for (uint32_t k = 0; k < K && !ok; ++k)
+                if (left[k] && deep_try(px, i, W, C, pred, dl[k])) { ok = 1; left[k] -= 1; total -= 1; }
         for (int tries = 0; tries < 48 && !ok && total; ++tries) {
             uint64_t r = ((uint64_t)XS() << 32 | XS()) % total;
             uint32_t k = 0;
             while (r >= left[k]) { r -= left[k]; ++k; }
-            int v[3], good = 1;
-            for (int c = 0; c < 3; ++c) {
-                v[c] = pred[c] + dl[k][c];
-                if (v[c] < 0 || v[c] > 255) good = 0;
-                /* drift back toward mid-range */
-                if ((pred[c] > 215 && dl[k][c] > 0) || (pred[c] < 40 && dl[k][c] < 0)) good = 0;
-            }
-            if (!good) continue;
-            for (int c = 0; c < 3; ++c) p[c] = (uint8_t)v[c];
-            /* coded (not a run member) and no back reference k = 1..4 */
-            const size_t q = i * C;
-            if (rgb_eq(px, q, q - C)) continue;
-            if (i >= W && rgb_eq(px, q, q - (size_t)W * C)) continue;
-            if (i >= W - 1 && W >= 1 && rgb_eq(px, q, q - (size_t)(W - 1) * C)) continue;
-            if (i >= 2 && rgb_eq(px, q, q - 2 * (size_t)C)) continue;
-            if (i >= 2 * (size_t)W && rgb_eq(px, q, q - 2 * (size_t)W * C)) continue;
+            if (!deep_try(px, i, W, C, pred, dl[k])) continue;
             ok = 1;
             left[k] -= 1;
             total -= 1;
@@ -1031,6 +1044,15 @@ void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C,
             for (int c = 0; c < 3; ++c) p[c] = (uint8_t)(pred[c] + 64 + 37 * c + (XS() & 15));
     }
 #undef XS
+}
+
+void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K) {
+    gen_deep(px, W, H, C, seed, K, NULL, 0);
+}
+
+void nice_oracle_gen_deep_codes_at(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
+                                   const uint64_t *force, size_t n_force) {
+    gen_deep(px, W, H, C, seed, K, force, n_force);
 }
 
 /* ------------------------------------------------------------------------- */

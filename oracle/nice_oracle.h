@@ -54,6 +54,9 @@ void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uin
 void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C);
 uint64_t nice_oracle_calc_pos_from(uint64_t width, uint64_t height, uint64_t index);
 void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K);
+/* as gen_deep_codes; pixels force[0..n_force) (ascending) take the rarest symbols */
+void nice_oracle_gen_deep_codes_at(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
+                                   const uint64_t *force, size_t n_force);
 
 #ifdef __cplusplus
 }

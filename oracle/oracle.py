@@ -101,6 +101,9 @@ def lib():
         L.nice_oracle_calc_pos_from.restype = ctypes.c_uint64
         L.nice_oracle_gen_deep_codes.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.nice_oracle_gen_deep_codes_at.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -182,6 +185,17 @@ def gen_deep_codes(width: int, height: int, channels: int, seed: int = 1, k: int
     up to about k-1 bits (test input for the long-code writer path)."""
     px = np.zeros(width * height * channels, dtype=np.uint8)
     lib().nice_oracle_gen_deep_codes(_u8p(px), width, height, channels, seed, k)
+    return px
+
+
+def gen_deep_codes_at(width: int, height: int, channels: int, seed: int, k: int, force) -> np.ndarray:
+    """gen_deep_codes whose pixels ``force`` (indices) take the rarest symbols
+    (longest codes) first: a band starting at such a pixel begins with a long
+    payload code."""
+    px = np.zeros(width * height * channels, dtype=np.uint8)
+    f = np.ascontiguousarray(sorted(force), dtype=np.uint64)
+    lib().nice_oracle_gen_deep_codes_at(_u8p(px), width, height, channels, seed, k,
+                                        f.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), f.size)
     return px
 
 

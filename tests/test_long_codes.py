@@ -95,3 +95,27 @@ def test_long_code_stream_decode_refused_cleanly(nice, O):
         O.decode(s, O.DEC_STRIDE)
     with pytest.raises(nice.NiceError):
         nice.decode_bytes(s)
+
+
+@pytest.mark.gpu
+def test_long_code_at_band_start(nice, O):
+    """Bands that start with a long payload code whose wrapped write covers the
+    previous band's last bits (the first code, a 1-bit prefix, leaves the
+    payload in band_bit0's byte): the write is deferred to the band's trailer
+    and applied after the merge; the stream is byte-exact."""
+    import torch
+    import importlib
+    from conftest import PKG_NAME
+    S = importlib.import_module(PKG_NAME + ".sharded")
+    w, h, c = 2560, 2400, 4
+    T = w * h // 1024
+    starts = list(range(100, T, 500))   # the rarest symbols sit at these tiles' first pixels
+    px = O.gen_deep_codes_at(w, h, c, 1, 31, [t * 1024 for t in starts])
+    want = O.encode(px, w, h, c)
+    bounds = [0] + starts + [T]
+    ranges = list(zip(bounds[:-1], bounds[1:]))
+    st = {}
+    got = S.encode_bands(torch.from_numpy(px).cuda(), w, h, c, len(ranges), ranges=ranges, stats=st)
+    assert st["deferred"], "no band started with a deferred wrapped write: move the split"
+    assert got.cpu().numpy().tobytes() == want
+
