@@ -43,12 +43,12 @@ def syn_lib():
     return _syn
 
 
-def syn_frames(torch, n, W, H, seed0, device):
-    """n NICE-SYN-v1 RGBA frames, seeds seed0 .. seed0+n-1,
-    generated on `device`: [n, W*H*4] uint8."""
-    out = torch.empty((n, W * H * 4), dtype=torch.uint8, device=device)
+def syn_frames(torch, n, W, H, seed0, device, channels=4):
+    """n NICE-SYN-v1 frames (RGBA, or RGB with channels=3),
+    seeds seed0 .. seed0+n-1, generated on `device`: [n, W*H*channels] uint8."""
+    out = torch.empty((n, W * H * channels), dtype=torch.uint8, device=device)
     st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
-    rc = syn_lib().nice_syn_v1_dev(ctypes.c_void_p(out.data_ptr()), out.stride(0), n, W, H, 4, seed0, st)
+    rc = syn_lib().nice_syn_v1_dev(ctypes.c_void_p(out.data_ptr()), out.stride(0), n, W, H, channels, seed0, st)
     if rc != 0:
         raise RuntimeError(f"nice_syn_v1_dev failed ({rc})")
     return out
@@ -151,7 +151,7 @@ def load_traffic(phase, frames, path=None):
     summary (bytes per frame from separate FETCH_SIZE / WRITE_SIZE passes,
     gfx950-corrected; see profiles/README.md), scaled to this launch's frame
     count; None if absent."""
-    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r02g.json")
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r03a.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -221,6 +221,46 @@ def config4_one_gpu(torch, nice, device, side, reps=3):
             "whole_frame_mpix_s": round(W * H / t_whole / 1e6, 1),
             "bands8_one_process_encode_ms": round(t_band * 1e3, 2),
             "band_stream_equals_whole_frame": bool(same), "stream_bytes": n}
+
+
+def rgb_leg(torch, nice, device, W, H, F, check, reps=3):
+    """4K RGB input (the reference CLI's common case, main.rs:39-41 ->
+    code.rs:59-64): F SYN-v1 RGB frames resident in HBM, encode-only and
+    decode-only rates; one stream byte-compared with the oracle and the round
+    trip checked (outside the timed regions)."""
+    N = W * H
+    px = syn_frames(torch, F, W, H, 5001, device, channels=3)
+    stride = (nice.encode_bound(W, H) + 255) // 256 * 256
+    streams = torch.empty((F, stride), dtype=torch.uint8, device=device)
+    lens = torch.zeros(F, dtype=torch.int64, device=device)
+    dec = torch.empty((F, N * 3), dtype=torch.uint8, device=device)
+    status = torch.zeros(F, dtype=torch.int32, device=device)
+    enc = lambda: nice.encode_batch(px, W, H, 3, streams, lens)
+    dcd = lambda: nice.decode_batch(streams, lens, W, H, 3, dec, status)
+    enc()
+    dcd()
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0 and torch.equal(dec, px), "RGB round trip"
+    exact = None
+    if check:
+        from oracle import oracle as O
+        want = O.encode(px[F - 1].cpu().numpy(), W, H, 3)
+        exact = streams[F - 1, :int(lens[F - 1])].cpu().numpy().tobytes() == want
+        assert exact, "RGB stream differs from the oracle"
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps
+    t_e, t_d = timed(enc), timed(dcd)
+    return {"workload": f"{F} x {W}x{H} RGB SYN-v1 frames (seeds 5001..), inputs resident in HBM",
+            "encode_mpix_s": round(F * N / t_e / 1e6, 1), "decode_mpix_s": round(F * N / t_d / 1e6, 1),
+            "encode_decode_mpix_s": round(F * N / (t_e + t_d) / 1e6, 1),
+            "bits_per_pixel": round(int(lens.sum()) * 8 / (F * N), 3),
+            "stream_check": None if exact is None else "oracle, last frame: byte-exact"}
 
 
 def gpu_numa_cpus(torch, device):
@@ -369,6 +409,8 @@ def main():
     ap.add_argument("--sharded-side", type=int, default=16384,
                     help="config 4: one side x side image encoded across the ranks (N>1), or whole and "
                          "in 8 bands on one GPU (N=1) (0: skip)")
+    ap.add_argument("--rgb-frames", type=int, default=128,
+                    help="4K RGB leg: frames per GPU encoded and decoded (0: skip)")
     ap.add_argument("--check-frames", type=int, default=4,
                     help="frames of the timed batch byte-compared with the oracle (rank 0)")
     ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
@@ -479,6 +521,14 @@ def main():
                 "gb_s": round(8 * N / t_pos / 1e9, 1), "frac": round(8 * N / t_pos / HBM_PEAK, 4)}
     del pos
 
+    rgb = None
+    if args.rgb_frames:
+        try:
+            rgb = rgb_leg(torch, nice, device, W, H, args.rgb_frames, rank == 0 and args.check_frames > 0)
+        except Exception as exc:   # report, never lose the main measurement
+            rgb = {"error": repr(exc)[:300]}
+        torch.cuda.empty_cache()
+
     stream_leg = None
     if args.streamed_frames:
         try:
@@ -551,6 +601,7 @@ def main():
         "single_frame_decode_ms": round(t_one_dec * 1e3, 3),
         "stream_check": check,
         "subblock_positions": subblock,
+        "rgb_4k": rgb,
         "stream_bytes_per_frame": stream_bytes // F,
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,

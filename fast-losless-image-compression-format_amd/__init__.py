@@ -327,13 +327,18 @@ class Pipeline:
         return [int(lens[i]) for i in range(n)]
 
     def decode(self, streams, lengths, outs, out_channels: int | None = None,
-               flags: int = DEC_ALPHA_FILL_FF):
-        """streams[f] (lengths[f] bytes) -> outs[f] (W*H*out_channels bytes)."""
+               flags: int = DEC_ALPHA_FILL_FF, raise_on_error: bool = True):
+        """streams[f] (lengths[f] bytes) -> outs[f] (W*H*out_channels bytes);
+        returns the per-frame statuses.  A frame's error raises NiceError unless
+        raise_on_error is False (outs[f] is undefined where status[f] != 0)."""
         n = len(streams)
         src = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(s) for s in streams])
         dst = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(o) for o in outs])
         ln = (ctypes.c_uint64 * max(n, 1))(*lengths)
         status = (ctypes.c_int32 * max(n, 1))()
         oc = self.channels if out_channels is None else out_channels
-        _check(lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status), "nice_pipe_decode")
-        return [int(status[i]) for i in range(n)]
+        rc = lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status)
+        st = [int(status[i]) for i in range(n)]
+        if rc != 0 and (raise_on_error or rc not in st):
+            _check(rc, "nice_pipe_decode")
+        return st

@@ -14,6 +14,14 @@
  * (Cargo.toml:16 panic = "abort").  Buffers are caller-owned.  Functions taking a
  * nice_ctx are thread-safe per context; the context-free functions use an
  * internal per-device context guarded by a mutex.
+ *
+ * Frame size cap: every encode/decode entry point (and the band API) refuses a
+ * frame of more than 2^30 pixels (w * h > 1073741824, e.g. 32768 x 32768) with
+ * NICE_E_ARG.  code::encode has no such limit (code.rs:59-64, 87); the cap keeps
+ * pixel indices and Huffman counts 32-bit on the device: a stream's symbol
+ * total is at most 3 per pixel (SC_RGB), i.e. < 3 * 2^30 < 2^32, which the
+ * heap's 32-bit count keys and merge sums hold exactly (tests/test_tables.py
+ * covers totals up to 3 * 2^30).  A 2^30-pixel RGBA frame is 4 GiB of input.
  */
 #ifndef NICE_H
 #define NICE_H
@@ -160,7 +168,10 @@ uint64_t nice_pipe_stream_stride(const nice_pipe* p);
 int nice_pipe_encode(nice_pipe* p, const uint8_t* const* px, uint32_t n_frames, uint8_t channels_out,
                      uint8_t* const* out, uint64_t out_cap, uint64_t* out_len);
 /* streams[f], stream_len[f] -> px[f] (w*h*out_channels bytes, out_channels <=
- * the pipe's channels); status[f] per frame (flags as nice_decode).  Blocks. */
+ * the pipe's channels); status[f] per frame (flags as nice_decode).  Blocks.
+ * px[f] is defined only where status[f] == NICE_OK: a chunk whose speculative
+ * parse had not settled when it was queued is copied out first and decoded
+ * again at slot reuse, so a frame that then fails may hold stale pixels. */
 int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, const uint64_t* stream_len, uint32_t n_frames,
                      uint8_t out_channels, uint8_t* const* px, uint32_t flags, int32_t* status);
 

@@ -75,3 +75,23 @@ def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
     for i in range(n):
         assert np.array_equal(dec[i].reshape(-1, c)[:, :3], frames[i].reshape(-1, c)[:, :3]), i
     p.close()
+
+
+def test_pipe_decode_unsettled_with_bad_stream(nice, O, monkeypatch):
+    """The redo path with an error in a redone chunk: every good frame exact,
+    the bad frame's status an error (its pixels are undefined, nice.h)."""
+    monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
+    w, h, c, n = 640, 480, 4, 5
+    frames = _frames(O, n, w, h, c, seed0=60)
+    p = nice.Pipeline(w, h, c, batch=2, depth=2)
+    outs = [np.zeros(p.stream_stride, np.uint8) for _ in range(n)]
+    lens = list(p.encode(frames, outs))
+    outs[3] = outs[3].copy()
+    outs[3][lens[3] // 2:lens[3]] ^= 0x5A          # corrupt the second half of frame 3's data
+    dec = [np.zeros(w * h * c, np.uint8) for _ in range(n)]
+    st = p.decode(outs, lens, dec, raise_on_error=False)
+    assert st[3] != 0
+    for i in (0, 1, 2, 4):
+        assert st[i] == 0, (i, st)
+        assert np.array_equal(dec[i].reshape(-1, c)[:, :3], frames[i].reshape(-1, c)[:, :3]), i
+    p.close()
