@@ -217,10 +217,24 @@ def config4_one_gpu(torch, nice, device, side, reps=3):
     t_band = (time.perf_counter() - t0) / reps
     n = int(ln[0])
     same = band.numel() == n and torch.equal(band, out[0, :n])
+    # its decode (replicas only across GPUs: one image's rows are one chain;
+    # several CUs per image through the strip-split row kernel)
+    del band
+    dec = torch.empty((1, W * H * 4), dtype=torch.uint8, device=device)
+    st = torch.zeros(1, dtype=torch.int32, device=device)
+    nice.decode_batch(out, ln, W, H, 4, dec, st, ctx=ctx)
+    torch.cuda.synchronize()
+    exact = int(st[0]) == 0 and torch.equal(dec.view(-1, 4)[:, :3], img.view(-1, 4)[:, :3])
+    t0 = time.perf_counter()
+    for _ in range(2):
+        nice.decode_batch(out, ln, W, H, 4, dec, st, ctx=ctx)
+    torch.cuda.synchronize()
+    t_dec = (time.perf_counter() - t0) / 2
     return {"workload": f"1 x {W}x{H} RGBA SYN-v1 image on 1 GPU", "whole_frame_encode_ms": round(t_whole * 1e3, 2),
             "whole_frame_mpix_s": round(W * H / t_whole / 1e6, 1),
             "bands8_one_process_encode_ms": round(t_band * 1e3, 2),
-            "band_stream_equals_whole_frame": bool(same), "stream_bytes": n}
+            "band_stream_equals_whole_frame": bool(same), "stream_bytes": n,
+            "whole_frame_decode_ms": round(t_dec * 1e3, 1), "decode_round_trip_exact": bool(exact)}
 
 
 def rgb_leg(torch, nice, device, W, H, F, check, reps=3):

@@ -396,12 +396,13 @@ struct DecLayout {
   size_t total;
   size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
   size_t o_ev, o_evck, o_evn, o_agree, o_items, o_icount;
+  size_t o_hand, o_abort;
 };
 // Jacobi iterations queued before the host first checks for the fixpoint (one
 // change flag each); further iterations, if any, check after every launch.
 constexpr uint32_t kSyncQueued = 6, kSyncFlags = 8;
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf,
-                     uint32_t ev_cap, uint32_t subs) {
+                     uint32_t ev_cap, uint32_t subs, size_t hand = 0) {
   DecLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -422,6 +423,8 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_agree = take(ev_cap ? (size_t)n_frames * max_chunks * 4 : 0);
   L.o_items = take(ev_cap ? (size_t)n_frames * max_chunks * subs * 4 : 0);
   L.o_icount = take(ev_cap ? (size_t)n_frames * 4 : 0);
+  L.o_hand = take(hand);
+  L.o_abort = take(hand ? (size_t)n_frames * 4 : 0);
   L.total = o;
   return L;
 }
@@ -559,7 +562,21 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
   const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
-  const size_t rowbuf = use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 17) * 4)
+  // wide frames, few of them: strips of <= 256 segments on separate CUs
+  // (dec_rows_split; every block must be resident: at most one per CU for
+  // half the CUs); NICE_DEC_SPLIT=k forces k strips (tests), =0 disables
+  const uint32_t nseg16 = (w + 15) / 16;
+  uint32_t strips = use_rows ? (nseg16 + SPLIT_THREADS_HOST - 1) / SPLIT_THREADS_HOST : 1;
+  if (const char* ev = getenv("NICE_DEC_SPLIT")) strips = (uint32_t)atoi(ev);
+  bool split = use_rows && strips >= 2 && (uint64_t)n_frames * strips <= (uint64_t)std::max(ctx->cus / 2, 1);
+  if (split) {
+    const uint32_t sps = (nseg16 + strips - 1) / strips;
+    // every strip >= 2 segments (>= 3 pixels: its first and last three) and <= 256 lanes
+    if (sps > SPLIT_THREADS_HOST || nseg16 <= (strips - 1) * sps + 1) split = false;
+  }
+  const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
+  const size_t rowbuf = split ? 0
+                      : use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 17) * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
   // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
   // a slice with more parses its events again in dec_emit) unless the scratch
@@ -570,12 +587,12 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     if (ev_cap && v >= 4 && v % 4 == 0 && v < ev_cap) ev_cap = v;
   }
   const uint32_t subs = cb / DEC_EMIT_BITS;
-  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, ev_cap, subs);
+  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, ev_cap, subs, hand);
   int rc = ctx->dec.grow(L.total);
   if (rc && ev_cap) {
     (void)hipGetLastError();   // the failed allocation
     ev_cap = 0;
-    L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, 0, subs);
+    L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, 0, subs, hand);
     rc = ctx->dec.grow(L.total);
   }
   if (rc) return rc;
@@ -703,7 +720,19 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     NICE_HIP(hipFuncSetAttribute((const void*)dec_reconstruct,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
   tm.begin(NICE_PH_DEC_RECON, st);
-  if (use_rows && rows_in_lds) {
+  if (split) {
+    a.strips = strips;
+    a.hand = (unsigned long long*)(base + L.o_hand);
+    a.hand_abort = (uint32_t*)(base + L.o_abort);
+    NICE_HIP(hipMemsetAsync(a.hand, 0, hand, st));
+    NICE_HIP(hipMemsetAsync(a.hand_abort, 0, (size_t)n_frames * 4, st));
+    const uint32_t sps = (nseg16 + strips - 1) / strips;
+    // tails + flags + 4, then the ring; above 80 KB so a CU holds one strip
+    size_t lds = ((size_t)SPLIT_THREADS_HOST * 7 + 4 + 4 * ((size_t)sps * 16 + 6 + ((sps * 16 + 6) >> 4) + 17)) * 4;
+    lds = std::max<size_t>(lds, 82 * 1024);
+    NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(dec_rows_split, dim3(n_frames * strips), dim3(SPLIT_THREADS_HOST), lds, st, a);
+  } else if (use_rows && rows_in_lds) {
     if (rows_lds > 64 * 1024)
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)rows_lds));

@@ -1834,6 +1834,407 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 __global__ __launch_bounds__(512) void dec_rows(DecArgs a) { dec_rows_body<512, true>(a); }
 __global__ __launch_bounds__(1024) void dec_rows_wide(DecArgs a) { dec_rows_body<1024, false>(a); }
 
+// ---------------------------------------------------------------------------
+// D5c: strip-split reconstruction for wide frames: a frame's row segments are
+// cut into k strips of <= 256 lanes, one workgroup each (one per CU), all rows
+// in order.  In raster order the strip-rows ("units" (y, j)) form one chain:
+// a unit's left neighbour is (y, j-1), or (y-1, k-1) for j = 0 (the wrap of
+// code.rs:412-413), its right neighbour (y, j+1), or (y+1, 0).  Each block
+// keeps a 4-row ring of its columns plus three halo columns on each side in
+// LDS; ring row r's left halo is the last three pixels of r's left neighbour
+// unit, its right halo the first three of r's right neighbour unit -- so every
+// reference (rows 1..3 back, +-3 pixels, code.rs:141-145) is one ring read
+// with no wrap logic, and lane 0's entry (the three pixels before the strip)
+// is ring row y's left halo.  Units publish their first and last three pixels
+// as soon as they are exact (after the speculative pass, usually without
+// their entry) as 8-byte {row + 1, value} granules (agent-scope relaxed
+// atomics: sc1 stores / loads); a block waits for nothing before its
+// speculative pass except the halos of rows y-2 and y-3 (published long
+// before); halo words of row y-1 not yet published and the entry are unknown
+// intervals in the speculative pass, resolved in the fix-up rounds, which poll
+// for them.  Every dependency points to a unit earlier in raster order, so
+// with every block resident (the host launches at most one block per CU for
+// half the CUs) the earliest unfinished unit always progresses.  Polls give up
+// after SPLIT_TIMEOUT (a frame-wide abort flag stops the other strips early
+// on an error).
+// ---------------------------------------------------------------------------
+constexpr uint32_t SPLIT_THREADS = 256;                      // lanes (16-pixel segments) per strip
+constexpr unsigned long long SPLIT_TIMEOUT = 400000000ull;   // s_memrealtime ticks (100 MHz): 4 s
+constexpr uint32_t SPLIT_GRAN = 8;                           // granules per unit: first3 at 0..2, last3 at 4..6
+__host__ __device__ constexpr uint32_t split_ring_stride(uint32_t sw) { return (sw + 6) + ((sw + 6) >> 4) + 17; }
+__device__ __forceinline__ uint32_t sr_idx(uint32_t lc3) { return lc3 + (lc3 >> 4); }
+
+__device__ __forceinline__ void hand_put(unsigned long long* p, uint32_t row, uint32_t v) {
+  __hip_atomic_store(p, ((unsigned long long)(row + 1u) << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long hand_get(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct SplitGeo {
+  uint32_t f, j, k, W, H, sw, RS;
+  unsigned long long* hand;   // frame f's granules
+  // granule i of unit (y, jj)
+  __device__ __forceinline__ unsigned long long* g(uint32_t y, uint32_t jj, uint32_t i) const {
+    return hand + ((uint64_t)y * k + jj) * SPLIT_GRAN + i;
+  }
+  // source granule of halo pixel i (0..2) of ring row r (>= -1: ring row -1's
+  // right halo is row 0's first pixels when j = k-1 -- pixel W-3 of row 0
+  // may reference pixel 0 through offset W-3), side 0 (left) / 1 (right);
+  // false when the source lies outside the image (never referenced)
+  __device__ __forceinline__ bool src(int r, uint32_t side, uint32_t i, unsigned long long*& p,
+                                      uint32_t& srow) const {
+    if (side == 0) {
+      if (j > 0) {
+        if (r < 0) return false;
+        p = g((uint32_t)r, j - 1, 4 + i); srow = (uint32_t)r; return true;
+      }
+      if (r < 1) return false;
+      p = g((uint32_t)r - 1, k - 1, 4 + i); srow = (uint32_t)r - 1; return true;
+    }
+    if (j + 1 < k) {
+      if (r < 0) return false;
+      p = g((uint32_t)r, j + 1, i); srow = (uint32_t)r; return true;
+    }
+    if (r < -1 || r + 1 >= (int)H) return false;
+    p = g((uint32_t)(r + 1), 0, i); srow = (uint32_t)(r + 1); return true;
+  }
+};
+
+// One poll of up to three halo items (ring row, side) by wave 0: lanes
+// 3t..3t+2 take item t's granules; an item whose three tags match is copied
+// into the ring and its LDS state word set to row + 2.  hv[slot * 2 + side]:
+// the ring row (>= -1) whose halo the slot holds, + 2 (0: none).  Callers
+// read hv after a barrier.
+__device__ __forceinline__ void halo_poll(const SplitGeo& G, uint32_t* ring, uint32_t* hv, uint32_t lane,
+                                          uint32_t n, const int* rows, const uint32_t* sides) {
+  if (lane >= 3u * n) return;
+  const uint32_t t = lane / 3u, i = lane - 3u * t;
+  const int r = rows[t];
+  const uint32_t side = sides[t];
+  uint32_t* st = hv + ((uint32_t)r & 3u) * 2u + side;
+  if (*st == (uint32_t)(r + 2)) return;
+  unsigned long long* p = nullptr;
+  uint32_t srow = 0;
+  const bool ex = G.src(r, side, i, p, srow);
+  const unsigned long long v = ex ? hand_get(p) : 0ull;
+  const bool ok = !ex || (uint32_t)(v >> 32) == srow + 1u;
+  const uint32_t lc3 = side ? G.sw + 3u + i : i;
+  if (ok) ring[((uint32_t)r & 3u) * G.RS + sr_idx(lc3)] = (uint32_t)v;
+  // the item's three lanes are consecutive lanes of wave 0
+  const unsigned long long m = __ballot(ok);
+  if (i == 0 && ((m >> lane) & 7ull) == 7ull) *st = (uint32_t)(r + 2);
+}
+
+__global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
+  constexpr int S = ROWS_SEG;
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  __shared__ uint32_t clsw[32];
+  __shared__ uint32_t hv[8];     // ring slot halo state (row + 1 per slot and side)
+  __shared__ uint32_t pend[2];
+  __shared__ int err;
+  const uint32_t k = a.strips;
+  const uint32_t f = blockIdx.x / k, j = blockIdx.x % k;
+  const uint32_t W = a.W, H = a.H;
+  const uint32_t nseg = (W + S - 1) / S;
+  const uint32_t sps = (nseg + k - 1) / k;
+  const uint32_t s0 = j * sps, s1 = min(nseg, s0 + sps);
+  const uint32_t c0 = s0 * S, sw = min(W, s1 * S) - c0;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nl = s1 - s0;
+  const bool active = lane < nl;
+  const uint32_t xl0 = lane * S;
+  const int nvalid = active ? (int)min((uint32_t)S, sw - xl0) : 0;
+  const SplitGeo G{f, j, k, W, H, sw, split_ring_stride(sw), a.hand + (uint64_t)f * H * k * SPLIT_GRAN};
+  const uint32_t RS = G.RS;
+  uint32_t* tails = sm;                              // SPLIT_THREADS x {lo, len} x 3
+  uint32_t* flags = tails + SPLIT_THREADS * 6;       // SPLIT_THREADS
+  uint32_t* ring = flags + SPLIT_THREADS + 4;        // 4 x RS
+  if (threadIdx.x < 32) {
+    const uint32_t c = threadIdx.x & 15u;
+    const unsigned long long kinds = threadIdx.x >= 16 ? ROWS_KIND_Y0 : ROWS_KIND;
+    clsw[threadIdx.x] = ((CLS_ROWS_PACK >> (2 * c)) & 3u) | (uint32_t)((CLS_PX_PACK >> (3 * c)) & 7u) << 2 |
+                        ((uint32_t)(kinds >> (4u * c)) & 15u) << 28;
+  }
+  if (threadIdx.x < 8) hv[threadIdx.x] = 0;
+  if (lane == 0) err = 0;
+  if (a.status[f] != 0) return;   // block-uniform
+  uint32_t* abort_f = a.hand_abort + f;
+  const uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + c0;
+  uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
+  const uint32_t OC = a.out_channels;
+  const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const bool vec_rec = ((W | c0) & 3u) == 0 && nvalid == S;
+  const bool vec_out = (OC == 4 && ((W | c0) & 3u) == 0 && nvalid == S) ||
+                       (OC == 3 && ((W | c0) & 15u) == 0 && nvalid == S);
+  uint32_t prev[S], rn[S];
+#pragma unroll
+  for (int p = 0; p < S; ++p) prev[p] = 0;
+  auto load_recs = [&](uint32_t y) {
+    const uint32_t* rrow = recs + (uint64_t)y * W + xl0;
+    if (vec_rec) {
+#pragma unroll
+      for (int q = 0; q < S / 4; ++q) {
+        const uint4 t = reinterpret_cast<const uint4*>(rrow)[q];
+        rn[4 * q] = t.x; rn[4 * q + 1] = t.y; rn[4 * q + 2] = t.z; rn[4 * q + 3] = t.w;
+      }
+    } else if (nvalid > 0) {
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = p < nvalid ? rrow[p] : REC_RUN;
+    } else {
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = REC_RUN;
+    }
+  };
+  if (H > 0) load_recs(0);
+  __syncthreads();
+  unsigned long long t_row = 0;   // when this row's waits began
+  // wave 0: gives up (error) on a timeout or another strip's abort
+  auto give_up = [&]() -> bool {
+    if (__hip_atomic_load(abort_f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if (lane == 0) atomicCAS(&err, 0, -1000);   // another strip failed: exit quietly
+      return true;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t_row > SPLIT_TIMEOUT) {
+      if (lane == 0) atomicCAS(&err, 0, NICE_E_HIP);
+      return true;
+    }
+    return false;
+  };
+  uint32_t y = 0;
+  for (; y < H; ++y) {
+    // ---- halos: rows y-2 and y-3 (wait), row y-1 and the entry (try)
+    t_row = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {   // slot y & 3 held row y-4: free it for row y
+      hv[(y & 3u) * 2u] = 0u;
+      hv[(y & 3u) * 2u + 1u] = 0u;
+    }
+    if (lane < 64) {
+      // ring rows y-2, y-3 (>= -1; a slot reset above holds none of them)
+      int rows[4];
+      uint32_t sides[4], n = 0;
+      for (int b = 2; b <= 3; ++b)
+        if ((int)y - b >= -1) { rows[n] = (int)y - b; sides[n++] = 0; rows[n] = (int)y - b; sides[n++] = 1; }
+      while (n) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        halo_poll(G, ring, hv, lane, n > 3 ? 3u : n, rows, sides);
+        if (n > 3) halo_poll(G, ring, hv, lane, 1, rows + 3, sides + 3);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        bool all = true;
+        for (uint32_t t = 0; t < n; ++t)
+          all = all && hv[((uint32_t)rows[t] & 3u) * 2u + sides[t]] == (uint32_t)(rows[t] + 2);
+        if (all) break;
+        if (give_up()) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (err == 0) {
+        int r2[3] = {(int)y - 1, (int)y - 1, (int)y};
+        uint32_t s2[3] = {0u, 1u, 0u};
+        halo_poll(G, ring, hv, lane, 3, r2, s2);
+      }
+    }
+    __syncthreads();
+    if (err) break;
+    const uint32_t ym1 = (y - 1u) & 3u;
+    bool hl1 = hv[ym1 * 2u] == y + 1u;               // row y-1's halos present (row -1 at y = 0)
+    bool hr1 = hv[ym1 * 2u + 1u] == y + 1u;
+    bool eok = hv[(y & 3u) * 2u] == y + 2u;          // the entry (row y's left halo)
+    // ---- pre-pass: records -> per-pixel words; a reference into a halo of
+    // row y-1 not yet present is marked W_CUR (unknown) with its halo slot
+    // (index in bits 8..9, side in bit 19) and resolved in the fix-up rounds
+    const uint32_t* const cwt = clsw + (y == 0 ? 16 : 0);
+    uint32_t w[S];
+    bool npend = false;
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+      const uint32_t r = rec_canon(rn[p], a.rec_tag);
+      const uint32_t cls = r >> 24;
+      const uint32_t cw = cwt[cls];
+      const uint32_t rows = cw & 3u;
+      const uint32_t lc3 = xl0 + (uint32_t)p + 6u - ((cw >> 2) & 7u);   // local column + 3 - pixels back
+      const bool up = cls >= 4;
+      const bool pl = up && rows == 1u && lc3 < 3u && !hl1;
+      const bool pr = up && rows == 1u && lc3 >= sw + 3u && !hr1;
+      const uint32_t lcc = min(lc3, sw + 5u);
+      const uint32_t o = ring[__umul24((y - rows) & 3u, RS) + sr_idx(lcc)];
+      const uint32_t c = spread3(r & 0xFFFFFFu);
+      const bool cur = pl || pr;
+      const uint32_t hslot = pl ? lc3 : (lc3 - sw - 3u);
+      const uint32_t kb = (cw & 0xF0000000u) | (cur ? W_CUR : 0u);
+      w[p] = kb | ((up && !cur) ? ((o + c) & SP_K) : c) | (cur ? ((hslot << 8) | (pr ? (1u << 19) : 0u)) : 0u);
+      npend = npend || cur;
+    }
+    // ---- entry: exact when present (strip 0 of row 0: zeros), else unknown
+    IvS r0{0u, SP_K}, r1{0u, SP_K}, r2{0u, SP_K};
+    if (lane == 0) {
+      if (y == 0 && j == 0) {
+        r0 = r1 = r2 = ivs_exact(0u);
+      } else if (eok) {
+        const uint32_t* hr = ring + (y & 3u) * RS;
+        r0 = ivs_exact(hr[sr_idx(2)]); r1 = ivs_exact(hr[sr_idx(1)]); r2 = ivs_exact(hr[sr_idx(0)]);
+      }
+    }
+    bool lane_exact = lane == 0 && ((y == 0 && j == 0) || eok);   // lane 0 started from its exact entry
+    if (y + 1 < H) load_recs(y + 1);
+    // ---- speculative pass
+    IvS v[S];
+    int lu = rows_spec<S>(v, r0, r1, r2, w, prev);
+    if (active) {
+      uint32_t* t = tails + lane * 6;
+      t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
+      t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
+      t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
+      flags[lane] = (lu < S - 3) ? 1u : 0u;
+    }
+    if (lane == 0) { pend[0] = 0; pend[1] = 0; }
+    bool fin = !active || lu < 0;
+    // the unit's first / last three pixels, published once exact
+    uint32_t pub = 0;
+    const bool pub_lane = active && (lane == 0 || xl0 + S + 3u > sw);
+    auto publish = [&]() {
+      if (!pub_lane) return;
+#pragma unroll
+      for (int p = 0; p < S; ++p) {
+        const uint32_t x = xl0 + (uint32_t)p;
+        const uint32_t il = x + 3u - sw;   // 0..2 for the last three pixels
+        if (x < 3u && !((pub >> x) & 1u) && v[p].len == 0u) {
+          hand_put(G.g(y, j, x), y, v[p].lo);
+          pub |= 1u << x;
+        }
+        if (x < sw && il < 3u && !((pub >> (4u + il)) & 1u) && v[p].len == 0u) {
+          hand_put(G.g(y, j, 4u + il), y, v[p].lo);
+          pub |= 16u << il;
+        }
+      }
+    };
+    publish();
+    rows_barrier<true>();
+    // ---- fix-up rounds (polling for the entry and row y-1's missing halos)
+    for (uint32_t rd = 0;; ++rd) {
+      if (!fin) atomicOr(&pend[rd & 1u], 1u);
+      if (lane < 64 && (!hl1 || !hr1 || !eok)) {
+        int r2[3];
+        uint32_t s2[3], m = 0;
+        if (!hl1) { r2[m] = (int)y - 1; s2[m++] = 0; }
+        if (!hr1) { r2[m] = (int)y - 1; s2[m++] = 1; }
+        if (!eok) { r2[m] = (int)y; s2[m++] = 0; }
+        halo_poll(G, ring, hv, lane, m, r2, s2);
+        if (rd > 0 && (rd & 3u) == 0u) __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane < 64 && (rd & 63u) == 63u) (void)give_up();   // bounds every wait (and any logic error)
+      rows_barrier<true>();
+      if (pend[rd & 1u] == 0 || err) break;
+      if (lane == 0) pend[(rd + 1) & 1u] = 0;
+      const bool nhl = hl1 || hv[ym1 * 2u] == y + 1u, nhr = hr1 || hv[ym1 * 2u + 1u] == y + 1u;
+      if (npend && ((nhl && !hl1) || (nhr && !hr1))) {
+        // halo words now present: resolve them (their chains are unknown from
+        // there on and get recomputed below)
+        const uint32_t* hrow = ring + ym1 * RS;
+        bool still = false;
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          if (w[p] & W_CUR) {
+            const uint32_t sd = (w[p] >> 19) & 1u, hs = (w[p] >> 8) & 3u;
+            if (sd ? nhr : nhl)
+              w[p] = (hrow[sr_idx(sd ? sw + 3u + hs : hs)] + (w[p] & SP_K)) & SP_K;
+            else
+              still = true;
+          }
+        }
+        npend = still;
+        if (!fin) { /* recompute below */ }
+      }
+      hl1 = nhl;
+      hr1 = nhr;
+      const bool neok = eok || hv[(y & 3u) * 2u] == y + 2u;
+      eok = neok;
+      bool exact_in = false;
+      bool go = !fin;
+      if (!fin) {
+        if (lane > 0) {
+          const uint32_t* t = tails + (lane - 1) * 6;
+          r0 = IvS{t[0], t[1]}; r1 = IvS{t[2], t[3]}; r2 = IvS{t[4], t[5]};
+          exact_in = flags[lane - 1] != 0;
+        } else if (eok) {
+          const uint32_t* hr = ring + (y & 3u) * RS;
+          r0 = ivs_exact(hr[sr_idx(2)]); r1 = ivs_exact(hr[sr_idx(1)]); r2 = ivs_exact(hr[sr_idx(0)]);
+          exact_in = true;
+        } else {
+          go = lane_exact;   // lane 0 without its entry: only halo words changed (else nothing to do)
+        }
+        exact_in = exact_in && !npend;
+      }
+      rows_barrier<true>();
+      if (__all(!go || exact_in))
+        lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
+      else
+        lu = rows_chain<S>(v, r0, r1, r2, w, prev, lu, go);
+      if (!fin) {
+        if (exact_in && lu >= 0) atomicCAS(&err, 0, NICE_E_FORMAT);
+        uint32_t* t = tails + lane * 6;
+        t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
+        t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
+        t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
+        flags[lane] = (lu < S - 3) ? 1u : 0u;
+        fin = (lu < 0 && !npend) || exact_in;
+        if (lane == 0 && exact_in) lane_exact = true;
+      }
+      publish();
+    }
+    if (err) break;
+    // ---- emit: ring row y (local columns) and the raster
+    if (active) {
+      uint32_t* rr = ring + (y & 3u) * RS;
+      const uint64_t pix = (uint64_t)y * W + c0 + xl0;
+#pragma unroll
+      for (int p = 0; p < S; ++p) rr[sr_idx(xl0 + (uint32_t)p + 3u)] = v[p].lo;   // padding: spare words
+      if (vec_out && OC == 4) {
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q)
+          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
+                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+      } else if (vec_out) {
+        uint32_t b[3 * S / 4];
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) {
+          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
+          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
+          b[3 * q] = u0 | (u1 << 24);
+          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
+          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+        }
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
+#pragma unroll
+        for (int q = 0; q < 3 * S / 16; ++q) o[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+      } else if (OC == 4) {
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(outp + pix * 4);
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+          if (p < nvalid) o32[p] = unspread3(v[p].lo) | alpha;
+      } else {
+        uint8_t* o8 = outp + pix * 3;
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          if (p < nvalid) {
+            const uint32_t u = unspread3(v[p].lo);
+            o8[3 * p] = (uint8_t)u; o8[3 * p + 1] = (uint8_t)(u >> 8); o8[3 * p + 2] = (uint8_t)(u >> 16);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < S; ++p) prev[p] = v[p].lo;
+    rows_barrier<true>();
+  }
+  if (lane == 0 && err) {
+    if (err != -1000) {
+      __hip_atomic_store(abort_f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      set_status(&a.status[f], err);
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void dec_reconstruct(DecArgs a) {
   if (a.rows_in_lds) dec_reconstruct_body<true>(a);
   else dec_reconstruct_body<false>(a);

@@ -155,6 +155,12 @@ struct DecArgs {
   uint32_t* agree;                    // n_frames * max_chunks: final parse == first pass from checkpoint agree-1 (0: entry)
   uint32_t* head_items;               // n_frames * max_chunks * (chunk_bits / DEC_EMIT_BITS): dec_emit's sub-slices
   uint32_t* head_count;               // n_frames: sub-slices listed
+  // dec_rows_split (wide frames, several workgroups per frame): strips per
+  // frame, the units' published first / last pixels (n_frames * H * strips *
+  // 8 granules, zeroed per call) and a per-frame abort flag
+  uint32_t strips;
+  unsigned long long* hand;
+  uint32_t* hand_abort;
 };
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
 // EV_RUN | pixels (saturated)
@@ -171,6 +177,9 @@ __global__ void dec_heads(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);
 __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);
+__global__ void dec_rows_split(DecArgs a);
+constexpr uint32_t SPLIT_THREADS_HOST = 256;   // == SPLIT_THREADS (nice_decode.hip): lanes per strip
+constexpr uint32_t SPLIT_GRAN_HOST = 8;        // == SPLIT_GRAN
 
 // Inclusive wave64 prefix sum by DPP: shifts 1, 2, 4, 8 inside each row of 16
 // lanes, then row 15 -> rows 1 and 3, row 31 -> rows 2 and 3.

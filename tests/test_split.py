@@ -1,0 +1,100 @@
+"""Strip-split row reconstruction (dec_rows_split): one wide frame decoded by
+several workgroups on separate CUs, each owning a strip of row segments and
+exchanging its first / last three pixels per row (the raster wrap of
+code.rs:412-413 and the +-3-pixel references of code.rs:141-145 cross strip
+edges).  Pixels must equal the oracle's decode for every strip count, partial
+last segments (W % 16 = 1, 2), long runs and reference chains crossing strips,
+RGB and RGBA; a corrupted stream must fail with a status, not hang.
+NICE_DEC_SPLIT=k forces k strips on frames narrow enough for one workgroup."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(O):
+    rng = np.random.default_rng(77)
+    cases = [
+        ("syn1000x40x3", O.gen_syn_v1(1000, 40, 3, 3), 1000, 40, 3),
+        ("syn1601x30x4", O.gen_syn_v1(1601, 30, 4, 4), 1601, 30, 4),   # W % 16 == 1
+        ("syn1058x25x3", O.gen_syn_v1(1058, 25, 3, 5), 1058, 25, 3),   # W % 16 == 2
+        ("grad800x64x3", O.gen_gradient(800, 64, 3), 800, 64, 3),
+    ]
+    st = np.zeros((60, 900, 3), np.uint8)          # runs across strips and rows
+    st[:, :, 0] = (np.arange(60)[:, None] // 7) * 20
+    st[::5, ::3, 1] = 200
+    cases.append(("stripes900x60x3", st.reshape(-1), 900, 60, 3))
+    pal = np.array([[10, 20, 30], [10, 21, 31], [200, 100, 50], [12, 22, 29]], np.uint8)
+    idx = rng.integers(0, 4, (50, 777))
+    idx[:, 300:500] = 2
+    cases.append(("palette777x50x3", pal[idx].reshape(-1), 777, 50, 3))
+    return cases
+
+
+def _check(nice, O, px, w, h, c):
+    s = O.encode(px, w, h, c)
+    got, img = nice.decode_bytes(s, flags=nice.DEC_ALPHA_FILL_FF | nice.DEC_TOLERANT_HEADER)
+    g = np.frombuffer(got, np.uint8).reshape(-1, c)
+    return np.array_equal(g[:, :3], px.reshape(-1, c)[:, :3])
+
+
+@pytest.mark.parametrize("k", [2, 3, 5])
+def test_split_forced_strips(nice, O, k, monkeypatch):
+    monkeypatch.setenv("NICE_DEC_SPLIT", str(k))
+    for name, px, w, h, c in _cases(O):
+        assert _check(nice, O, px, w, h, c), (name, k)
+
+
+def test_split_default_wide(nice, O, monkeypatch):
+    """W > 4096 splits by default (ceil(W / 16 / 256) strips); =0 disables."""
+    px = O.gen_syn_v1(8200, 9, 4, 8)
+    assert _check(nice, O, px, 8200, 9, 4)
+    monkeypatch.setenv("NICE_DEC_SPLIT", "0")
+    assert _check(nice, O, px, 8200, 9, 4)
+
+
+def test_split_batch_rgb_out(nice, O, monkeypatch):
+    """A batch (several frames, each split) through the device API, RGBA
+    streams decoded to 3-channel output."""
+    import torch
+    monkeypatch.setenv("NICE_DEC_SPLIT", "3")
+    w, h, c, n = 1200, 20, 4, 5
+    frames = [O.gen_syn_v1(w, h, c, 30 + i) for i in range(n)]
+    streams = [O.encode(f, w, h, c) for f in frames]
+    stride = (max(len(s) for s in streams) + 255) // 256 * 256
+    sb = torch.zeros((n, stride), dtype=torch.uint8)
+    for i, s in enumerate(streams):
+        sb[i, :len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
+    sb = sb.cuda()
+    lens = torch.tensor([len(s) for s in streams], dtype=torch.int64, device="cuda")
+    dec = torch.zeros((n, w * h * 3), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(n, dtype=torch.int32, device="cuda")
+    nice.decode_batch(sb, lens, w, h, 3, dec, status, flags=nice.DEC_TOLERANT_HEADER)
+    torch.cuda.synchronize()
+    assert status.cpu().tolist() == [0] * n
+    for i in range(n):
+        assert np.array_equal(dec[i].cpu().numpy(), frames[i].reshape(-1, 4)[:, :3].reshape(-1)), i
+
+
+def test_split_corrupt_stream_fails_fast(nice, O, monkeypatch):
+    """A stream whose records reference outside the image or mis-parse: the
+    split decode reports an error (or decodes) without waiting on a strip that
+    stopped -- it returns well inside the per-row poll timeout."""
+    monkeypatch.setenv("NICE_DEC_SPLIT", "4")
+    w, h, c = 1500, 30, 3
+    px = O.gen_syn_v1(w, h, c, 12)
+    s = bytearray(O.encode(px, w, h, c))
+    rng = np.random.default_rng(5)
+    for trial in range(6):
+        t = bytearray(s)
+        for pos in rng.integers(800, len(t), 8):
+            t[pos] ^= 0xFF
+        t0 = time.time()
+        try:
+            nice.decode_bytes(bytes(t), flags=nice.DEC_ALPHA_FILL_FF | nice.DEC_TOLERANT_HEADER)
+        except nice.NiceError:
+            pass
+        assert time.time() - t0 < 3.0, trial
+    assert _check(nice, O, px, w, h, c)   # the context still decodes afterwards
