@@ -1901,29 +1901,53 @@ struct SplitGeo {
   }
 };
 
-// One poll of up to three halo items (ring row, side) by wave 0: lanes
-// 3t..3t+2 take item t's granules; an item whose three tags match is copied
-// into the ring and its LDS state word set to row + 2.  hv[slot * 2 + side]:
-// the ring row (>= -1) whose halo the slot holds, + 2 (0: none).  Callers
-// read hv after a barrier.
-__device__ __forceinline__ void halo_poll(const SplitGeo& G, uint32_t* ring, uint32_t* hv, uint32_t lane,
-                                          uint32_t n, const int* rows, const uint32_t* sides) {
-  if (lane >= 3u * n) return;
-  const uint32_t t = lane / 3u, i = lane - 3u * t;
-  const int r = rows[t];
-  const uint32_t side = sides[t];
-  uint32_t* st = hv + ((uint32_t)r & 3u) * 2u + side;
-  if (*st == (uint32_t)(r + 2)) return;
-  unsigned long long* p = nullptr;
-  uint32_t srow = 0;
-  const bool ex = G.src(r, side, i, p, srow);
-  const unsigned long long v = ex ? hand_get(p) : 0ull;
-  const bool ok = !ex || (uint32_t)(v >> 32) == srow + 1u;
-  const uint32_t lc3 = side ? G.sw + 3u + i : i;
-  if (ok) ring[((uint32_t)r & 3u) * G.RS + sr_idx(lc3)] = (uint32_t)v;
-  // the item's three lanes are consecutive lanes of wave 0
-  const unsigned long long m = __ballot(ok);
-  if (i == 0 && ((m >> lane) & 7ull) == 7ull) *st = (uint32_t)(r + 2);
+// A wave-0 poll in two halves, so the granule loads' latency overlaps other
+// work.  The halo items of row y: t = 0..5 ring rows y-3, y-3, y-2, y-2, y-1,
+// y-1 (left, right), t = 6 row y's left halo (the entry); lanes 3t..3t+2 take
+// item t.  issue() loads the granules of the items in `mask` whose hv word
+// does not say present; commit() copies every item whose three tags match
+// into the ring and sets its hv word.  hv[slot * 2 + side]: the ring row
+// (>= -1) whose halo the slot holds, + 2 (0: none).
+struct HaloPoll {
+  unsigned long long v;
+  int r;
+  uint32_t side, i, srow;   // side 2: no item on this lane
+  bool ex;
+  __device__ __forceinline__ void issue(const SplitGeo& G, const uint32_t* hv, uint32_t lane, uint32_t y,
+                                        uint32_t mask) {
+    side = 2u;
+    ex = false;
+    v = 0;
+    const uint32_t t = lane / 3u;
+    i = lane - 3u * t;
+    if (t >= 7u || !((mask >> t) & 1u)) return;
+    const int rr = t < 6u ? (int)y - 3 + (int)(t >> 1) : (int)y;
+    const uint32_t sd = t < 6u ? (t & 1u) : 0u;
+    if (rr < -1 || hv[((uint32_t)rr & 3u) * 2u + sd] == (uint32_t)(rr + 2)) return;
+    r = rr;
+    side = sd;
+    unsigned long long* p = nullptr;
+    ex = G.src(rr, sd, i, p, srow);
+    if (ex) v = hand_get(p);
+  }
+  __device__ __forceinline__ void commit(const SplitGeo& G, uint32_t* ring, uint32_t* hv, uint32_t lane) {
+    const bool ok = side < 2u && (!ex || (uint32_t)(v >> 32) == srow + 1u);
+    if (ok) ring[((uint32_t)r & 3u) * G.RS + sr_idx(side ? G.sw + 3u + i : i)] = (uint32_t)v;
+    const unsigned long long m = __ballot(ok);
+    if (ok && i == 0u && ((m >> lane) & 7ull) == 7ull) hv[((uint32_t)r & 3u) * 2u + side] = (uint32_t)(r + 2);
+    side = 2u;
+  }
+};
+// present bits (t = 0..6) of row y's halo items
+__device__ __forceinline__ uint32_t halo_have(const uint32_t* hv, uint32_t y) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 7u; ++t) {
+    const int rr = t < 6u ? (int)y - 3 + (int)(t >> 1) : (int)y;
+    const uint32_t sd = t < 6u ? (t & 1u) : 0u;
+    if (rr < -1 || hv[((uint32_t)rr & 3u) * 2u + sd] == (uint32_t)(rr + 2)) m |= 1u << t;
+  }
+  return m;
 }
 
 __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
@@ -2001,8 +2025,19 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     }
     return false;
   };
+  HaloPoll HP;
+  bool pending_poll = false;   // wave 0: HP holds issued loads
+  // timing counters (NICE_DEC_STATS=1) only in -DNICE_ROWS_STATS builds
+#ifdef NICE_ROWS_STATS
+  unsigned long long* const stats = a.stats;
+#else
+  constexpr unsigned long long* stats = nullptr;
+#endif
+  unsigned long long c_entry = 0, c_right = 0;
+  unsigned long long c_wait = 0, c_spec = 0, c_fix = 0, c_emit = 0, n_rounds = 0, n_polls = 0, n_noentry = 0;
   uint32_t y = 0;
   for (; y < H; ++y) {
+    const unsigned long long cc0 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- halos: rows y-2 and y-3 (wait), row y-1 and the entry (try)
     t_row = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {   // slot y & 3 held row y-4: free it for row y
@@ -2010,27 +2045,19 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
       hv[(y & 3u) * 2u + 1u] = 0u;
     }
     if (lane < 64) {
-      // ring rows y-2, y-3 (>= -1; a slot reset above holds none of them)
-      int rows[4];
-      uint32_t sides[4], n = 0;
-      for (int b = 2; b <= 3; ++b)
-        if ((int)y - b >= -1) { rows[n] = (int)y - b; sides[n++] = 0; rows[n] = (int)y - b; sides[n++] = 1; }
-      while (n) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        halo_poll(G, ring, hv, lane, n > 3 ? 3u : n, rows, sides);
-        if (n > 3) halo_poll(G, ring, hv, lane, 1, rows + 3, sides + 3);
+      // the loads issued at the end of the previous row, then rows y-2 and
+      // y-3 (items 0..3) until present
+      if (pending_poll) HP.commit(G, ring, hv, lane);
+      pending_poll = false;
+      while (true) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        bool all = true;
-        for (uint32_t t = 0; t < n; ++t)
-          all = all && hv[((uint32_t)rows[t] & 3u) * 2u + sides[t]] == (uint32_t)(rows[t] + 2);
-        if (all) break;
+        const uint32_t miss = ~halo_have(hv, y) & 15u;
+        if (!miss) break;
         if (give_up()) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (err == 0) {
-        int r2[3] = {(int)y - 1, (int)y - 1, (int)y};
-        uint32_t s2[3] = {0u, 1u, 0u};
-        halo_poll(G, ring, hv, lane, 3, r2, s2);
+        HP.issue(G, hv, lane, y, miss);
+        HP.commit(G, ring, hv, lane);
+        if (stats) ++n_polls;
+        __builtin_amdgcn_s_sleep(1);
       }
     }
     __syncthreads();
@@ -2039,6 +2066,8 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     bool hl1 = hv[ym1 * 2u] == y + 1u;               // row y-1's halos present (row -1 at y = 0)
     bool hr1 = hv[ym1 * 2u + 1u] == y + 1u;
     bool eok = hv[(y & 3u) * 2u] == y + 2u;          // the entry (row y's left halo)
+    const unsigned long long cc1 = stats ? __builtin_amdgcn_s_memtime() : 0;
+    if (stats && !eok) ++n_noentry;
     // ---- pre-pass: records -> per-pixel words; a reference into a halo of
     // row y-1 not yet present is marked W_CUR (unknown) with its halo slot
     // (index in bits 8..9, side in bit 19) and resolved in the fix-up rounds
@@ -2074,7 +2103,6 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
         r0 = ivs_exact(hr[sr_idx(2)]); r1 = ivs_exact(hr[sr_idx(1)]); r2 = ivs_exact(hr[sr_idx(0)]);
       }
     }
-    bool lane_exact = lane == 0 && ((y == 0 && j == 0) || eok);   // lane 0 started from its exact entry
     if (y + 1 < H) load_recs(y + 1);
     // ---- speculative pass
     IvS v[S];
@@ -2088,6 +2116,9 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     }
     if (lane == 0) { pend[0] = 0; pend[1] = 0; }
     bool fin = !active || lu < 0;
+    // the entry the lane last computed from: a fix-up round recomputes only
+    // when it changed (or halo words were resolved)
+    uint32_t q0 = r0.lo, q1 = r0.len, q2 = r1.lo, q3 = r1.len, q4 = r2.lo, q5 = r2.len;
     // the unit's first / last three pixels, published once exact
     uint32_t pub = 0;
     const bool pub_lane = active && (lane == 0 || xl0 + S + 3u > sw);
@@ -2109,24 +2140,32 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     };
     publish();
     rows_barrier<true>();
+    const unsigned long long cc2 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- fix-up rounds (polling for the entry and row y-1's missing halos)
     for (uint32_t rd = 0;; ++rd) {
+      if (stats) ++n_rounds;
       if (!fin) atomicOr(&pend[rd & 1u], 1u);
-      if (lane < 64 && (!hl1 || !hr1 || !eok)) {
-        int r2[3];
-        uint32_t s2[3], m = 0;
-        if (!hl1) { r2[m] = (int)y - 1; s2[m++] = 0; }
-        if (!hr1) { r2[m] = (int)y - 1; s2[m++] = 1; }
-        if (!eok) { r2[m] = (int)y; s2[m++] = 0; }
-        halo_poll(G, ring, hv, lane, m, r2, s2);
-        if (rd > 0 && (rd & 3u) == 0u) __builtin_amdgcn_s_sleep(1);
+      if (lane < 64) {
+        // commit the loads issued last round, issue the still missing items
+        // (row y-1's halos, the entry); their latency overlaps this round
+        if (pending_poll) HP.commit(G, ring, hv, lane);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        const uint32_t miss = ~halo_have(hv, y) & 0x70u;
+        pending_poll = miss != 0u;
+        if (pending_poll) {
+          HP.issue(G, hv, lane, y, miss);
+          if (stats) ++n_polls;
+          if (rd > 1u) __builtin_amdgcn_s_sleep(1);
+        }
       }
       if (lane < 64 && (rd & 63u) == 63u) (void)give_up();   // bounds every wait (and any logic error)
       rows_barrier<true>();
       if (pend[rd & 1u] == 0 || err) break;
       if (lane == 0) pend[(rd + 1) & 1u] = 0;
       const bool nhl = hl1 || hv[ym1 * 2u] == y + 1u, nhr = hr1 || hv[ym1 * 2u + 1u] == y + 1u;
+      bool resolved = false;
       if (npend && ((nhl && !hl1) || (nhr && !hr1))) {
+        resolved = true;
         // halo words now present: resolve them (their chains are unknown from
         // there on and get recomputed below)
         const uint32_t* hrow = ring + ym1 * RS;
@@ -2147,6 +2186,8 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
       hl1 = nhl;
       hr1 = nhr;
       const bool neok = eok || hv[(y & 3u) * 2u] == y + 2u;
+      if (stats && neok && !eok) c_entry += __builtin_amdgcn_s_memtime() - cc2;
+      if (stats && nhr && !hr1) c_right += __builtin_amdgcn_s_memtime() - cc2;
       eok = neok;
       bool exact_in = false;
       bool go = !fin;
@@ -2160,16 +2201,19 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
           r0 = ivs_exact(hr[sr_idx(2)]); r1 = ivs_exact(hr[sr_idx(1)]); r2 = ivs_exact(hr[sr_idx(0)]);
           exact_in = true;
         } else {
-          go = lane_exact;   // lane 0 without its entry: only halo words changed (else nothing to do)
+          r0 = IvS{q0, q1}; r1 = IvS{q2, q3}; r2 = IvS{q4, q5};   // lane 0 without its entry: as before
         }
         exact_in = exact_in && !npend;
+        const bool same = r0.lo == q0 && r0.len == q1 && r1.lo == q2 && r1.len == q3 && r2.lo == q4 && r2.len == q5;
+        go = !same || resolved;
+        q0 = r0.lo; q1 = r0.len; q2 = r1.lo; q3 = r1.len; q4 = r2.lo; q5 = r2.len;
       }
       rows_barrier<true>();
       if (__all(!go || exact_in))
         lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
       else
         lu = rows_chain<S>(v, r0, r1, r2, w, prev, lu, go);
-      if (!fin) {
+      if (go) {
         if (exact_in && lu >= 0) atomicCAS(&err, 0, NICE_E_FORMAT);
         uint32_t* t = tails + lane * 6;
         t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
@@ -2177,11 +2221,17 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
         t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
         flags[lane] = (lu < S - 3) ? 1u : 0u;
         fin = (lu < 0 && !npend) || exact_in;
-        if (lane == 0 && exact_in) lane_exact = true;
       }
       publish();
     }
     if (err) break;
+    // prefetch the next row's halo items (committed at its start)
+    if (lane < 64 && y + 1 < H) {
+      if (pending_poll) HP.commit(G, ring, hv, lane);
+      HP.issue(G, hv, lane, y + 1, 0x7Fu);
+      pending_poll = true;
+    }
+    const unsigned long long cc3 = stats ? __builtin_amdgcn_s_memtime() : 0;
     // ---- emit: ring row y (local columns) and the raster
     if (active) {
       uint32_t* rr = ring + (y & 3u) * RS;
@@ -2226,6 +2276,16 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
 #pragma unroll
     for (int p = 0; p < S; ++p) prev[p] = v[p].lo;
     rows_barrier<true>();
+    if (stats) {
+      const unsigned long long cc4 = __builtin_amdgcn_s_memtime();
+      c_wait += cc1 - cc0; c_spec += cc2 - cc1; c_fix += cc3 - cc2; c_emit += cc4 - cc3;
+    }
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], (unsigned long long)y); atomicAdd(&stats[4], n_rounds);
+    atomicAdd(&stats[5], c_wait); atomicAdd(&stats[6], c_spec); atomicAdd(&stats[7], c_fix);
+    atomicAdd(&stats[8], c_emit); atomicAdd(&stats[1], n_noentry); atomicAdd(&stats[2], n_polls);
+    atomicAdd(&stats[3], c_entry); atomicAdd(&stats[9], c_right);
   }
   if (lane == 0 && err) {
     if (err != -1000) {
