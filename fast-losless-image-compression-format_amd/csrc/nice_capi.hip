@@ -562,6 +562,16 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
   const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
+  // 8-pixel segments, twice the lanes per frame, where 16-pixel segments
+  // would leave SIMDs of a frame's CU idle (W <= 2048: at most two waves) and
+  // frames do not share CUs: 64 x 1080p 7.83 -> 6.32 ms; slower at 4K (four
+  // waves already: single frame 16.1 -> 17.7 ms).  NICE_DEC_SEG=8/16 forces a size
+  const uint32_t rows8_thr = ((w + 7) / 8 + 63) / 64 * 64;
+  const size_t rows8_lds = ((size_t)rows8_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;
+  bool rows8 = use_rows && rows_in_lds && rows_thr <= 128 && rows8_thr <= 512 && rows8_lds <= 160 * 1024 &&
+               n_frames <= (uint32_t)ctx->cus;
+  if (const char* ev = getenv("NICE_DEC_SEG")) rows8 = atoi(ev) == 8 && use_rows && rows_in_lds &&
+                                                       rows8_thr <= 512 && rows8_lds <= 160 * 1024;
   // wide frames, few of them: strips of <= 256 segments on separate CUs
   // (dec_rows_split; every block must be resident: at most one per CU for
   // half the CUs); NICE_DEC_SPLIT=k forces k strips (tests), =0 disables
@@ -732,6 +742,11 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     lds = std::max<size_t>(lds, 82 * 1024);
     NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(dec_rows_split, dim3(n_frames * strips), dim3(SPLIT_THREADS_HOST), lds, st, a);
+  } else if (use_rows && rows_in_lds && rows8) {
+    if (rows8_lds > 64 * 1024)
+      NICE_HIP(hipFuncSetAttribute((const void*)dec_rows8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)rows8_lds));
+    hipLaunchKernelGGL(dec_rows8, dim3(n_frames), dim3(rows8_thr), rows8_lds, st, a);
   } else if (use_rows && rows_in_lds) {
     if (rows_lds > 64 * 1024)
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1638,9 +1638,8 @@ __device__ __forceinline__ void rows_barrier() {
 // partial last segment's padding pixels (stored unmasked).
 __host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 17; }
 
-template <int MAXT, bool LDS_RING>
+template <int MAXT, bool LDS_RING, int S = ROWS_SEG>
 __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
-  constexpr int S = ROWS_SEG;
   // diagnostics counters (NICE_DEC_STATS=1) only in -DNICE_ROWS_STATS builds:
   // the runtime checks alone held SGPRs and branches in the row loop
 #ifdef NICE_ROWS_STATS
@@ -1682,7 +1681,8 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   const uint32_t OC = a.out_channels;
   const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
   const bool vec_rec = (W & 3u) == 0 && nvalid == S;
-  const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) || (OC == 3 && (W & 15u) == 0 && nvalid == S);
+  const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) ||
+                       (OC == 3 && S % 16 == 0 && (W & 15u) == 0 && nvalid == S);
   if (lane == 0) *err = 0;
   uint32_t prev[S], rn[S];
 #pragma unroll
@@ -1823,18 +1823,20 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
           o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
                             unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
       } else if (vec_out) {
-        uint32_t b[3 * S / 4];
+        if constexpr (S % 16 == 0) {
+          uint32_t b[3 * S / 4];
 #pragma unroll
-        for (int q = 0; q < S / 4; ++q) {
-          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
-          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
-          b[3 * q] = u0 | (u1 << 24);
-          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
-          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+          for (int q = 0; q < S / 4; ++q) {
+            const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
+            const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
+            b[3 * q] = u0 | (u1 << 24);
+            b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
+            b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+          }
+          uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
+#pragma unroll
+          for (int q = 0; q < 3 * S / 16; ++q) o[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
         }
-        uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
-#pragma unroll
-        for (int q = 0; q < 3 * S / 16; ++q) o[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
       } else if (OC == 4) {
         uint32_t* o32 = reinterpret_cast<uint32_t*>(outp + pix * 4);
 #pragma unroll
@@ -1871,6 +1873,9 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 // Ring in LDS (4 rows fit next to the block's tails) or in global memory.
 __global__ __launch_bounds__(512) void dec_rows(DecArgs a) { dec_rows_body<512, true>(a); }
 __global__ __launch_bounds__(1024) void dec_rows_wide(DecArgs a) { dec_rows_body<1024, false>(a); }
+// 8-pixel segments (W <= 4096: up to 512 lanes): twice the lanes per frame,
+// for batches too small to fill the CUs (single-frame latency)
+__global__ __launch_bounds__(512) void dec_rows8(DecArgs a) { dec_rows_body<512, true, 8>(a); }
 
 // ---------------------------------------------------------------------------
 // D5c: strip-split reconstruction for wide frames: a frame's row segments are

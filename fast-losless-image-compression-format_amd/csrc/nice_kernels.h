@@ -177,6 +177,7 @@ __global__ void dec_heads(DecArgs a);
 __global__ void dec_reconstruct(DecArgs a);
 __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);
+__global__ void dec_rows8(DecArgs a);
 __global__ void dec_rows_split(DecArgs a);
 constexpr uint32_t SPLIT_THREADS_HOST = 256;   // == SPLIT_THREADS (nice_decode.hip): lanes per strip
 constexpr uint32_t SPLIT_GRAN_HOST = 8;        // == SPLIT_GRAN
