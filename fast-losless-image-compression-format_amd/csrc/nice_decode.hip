@@ -1790,18 +1790,20 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         exact_in = flags[lane - 1] != 0;
       }
       rows_barrier<LDS_RING>();
-      if (__all(fin || exact_in))   // wave-uniform: every recomputing lane has exact inputs
-        lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, !fin);
-      else
-        lu = rows_chain<S>(v, r0, r1, r2, w, prev, lu, !fin);
-      if (!fin) {
-        if (exact_in && lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
+      // only lanes whose left tail is exact recompute, with plain arithmetic:
+      // refining from an inexact neighbour (interval chain) rarely collapses
+      // anything in one round and forced its whole wave onto the interval
+      // chain; the leftmost unfinished lane always has an exact left tail
+      const bool go = !fin && exact_in;
+      lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
+      if (go) {
+        if (lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
         uint32_t* t = tails + lane * 6;
         t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
         t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
         t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
-        flags[lane] = (lu < S - 3) ? 1u : 0u;
-        fin = lu < 0 || exact_in;
+        flags[lane] = 1u;
+        fin = true;
       }
     }
     if (stats && lane == 0) {
@@ -2159,9 +2161,6 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     }
     if (lane == 0) { pend[0] = 0; pend[1] = 0; }
     bool fin = !active || lu < 0;
-    // the entry the lane last computed from: a fix-up round recomputes only
-    // when it changed (or halo words were resolved)
-    uint32_t q0 = r0.lo, q1 = r0.len, q2 = r1.lo, q3 = r1.len, q4 = r2.lo, q5 = r2.len;
     // the unit's first / last three pixels, published once exact
     uint32_t pub = 0;
     const bool pub_lane = active && (lane == 0 || xl0 + S + 3u > sw);
@@ -2243,27 +2242,22 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
           const uint32_t* hr = ring + (y & 3u) * RS;
           r0 = ivs_exact(hr[sr_idx(2)]); r1 = ivs_exact(hr[sr_idx(1)]); r2 = ivs_exact(hr[sr_idx(0)]);
           exact_in = true;
-        } else {
-          r0 = IvS{q0, q1}; r1 = IvS{q2, q3}; r2 = IvS{q4, q5};   // lane 0 without its entry: as before
         }
         exact_in = exact_in && !npend;
-        const bool same = r0.lo == q0 && r0.len == q1 && r1.lo == q2 && r1.len == q3 && r2.lo == q4 && r2.len == q5;
-        go = !same || resolved;
-        q0 = r0.lo; q1 = r0.len; q2 = r1.lo; q3 = r1.len; q4 = r2.lo; q5 = r2.len;
+        // as in dec_rows: only exact left tails (or entries) are used
+        go = exact_in;
       }
+      (void)resolved;
       rows_barrier<true>();
-      if (__all(!go || exact_in))
-        lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
-      else
-        lu = rows_chain<S>(v, r0, r1, r2, w, prev, lu, go);
+      lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
       if (go) {
-        if (exact_in && lu >= 0) atomicCAS(&err, 0, NICE_E_FORMAT);
+        if (lu >= 0) atomicCAS(&err, 0, NICE_E_FORMAT);
         uint32_t* t = tails + lane * 6;
         t[0] = v[S - 1].lo; t[1] = v[S - 1].len;
         t[2] = v[S - 2].lo; t[3] = v[S - 2].len;
         t[4] = v[S - 3].lo; t[5] = v[S - 3].len;
-        flags[lane] = (lu < S - 3) ? 1u : 0u;
-        fin = (lu < 0 && !npend) || exact_in;
+        flags[lane] = 1u;
+        fin = true;
       }
       publish();
     }
