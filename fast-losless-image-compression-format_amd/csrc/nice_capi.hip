@@ -104,7 +104,7 @@ int check_device(int device) {
 static const char* kPhaseNames[NICE_PHASES] = {
     "enc_classify", "enc_tailruns", "enc_tables", "enc_header", "enc_tilebits", "enc_tilescan",
     "enc_pack", "enc_tail", "enc_pack_long", "dec_tables", "dec_sync", "dec_scan", "dec_emit",
-    "dec_reconstruct", "dec_place"};
+    "dec_reconstruct", "dec_place", "dec_resync"};
 
 // Optional per-phase HIP-event timing (bench / profiling).
 struct PhaseTimer {
@@ -679,7 +679,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
   for (uint32_t it = 0; it < queued; ++it, ++it_count) {
-    tm.begin(NICE_PH_DEC_SYNC, st);
+    tm.begin(it ? NICE_PH_DEC_RESYNC : NICE_PH_DEC_SYNC, st);
     hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
     tm.end(st);
   }
@@ -693,7 +693,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   for (uint32_t it = queued; host_changed && it < max_it; ++it, ++it_count) {
     NICE_HIP(hipMemsetAsync(changed + kSyncFlags - 1, 0, 4, st));
-    tm.begin(NICE_PH_DEC_SYNC, st);
+    tm.begin(NICE_PH_DEC_RESYNC, st);
     hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + kSyncFlags - 1, nullptr);
     tm.end(st);
     NICE_HIP(hipMemcpyAsync(&host_changed, changed + kSyncFlags - 1, 4, hipMemcpyDeviceToHost, st));

@@ -1551,7 +1551,20 @@ __device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uin
   return IvS{(va.lo & ma) | (rlo & ~ma), (va.len & ma) | (slen & ~ma)};
 }
 
+// rows_chain when every input is exact (r0..r2 and the kept pixels): plain
+// arithmetic, no intervals.  Only after the W_CUR words are resolved.
+__device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, uint32_t l3, uint32_t u,
+                                                    uint32_t wp) {
+  const uint32_t c = wp & SP_K;
+  const uint32_t va = ((((l1 + u) >> 1) & SP_K) + c) & SP_K;
+  const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
+  const uint32_t rlo = (sel + c) & SP_K;
+  return (wp & W_AVG) ? va : rlo;
+}
+
 // Speculative pass over the whole segment; returns the last unknown index.
+// (Switching a wave to the plain step once all its lanes are exact -- one
+// vote per pixel -- was 5 % slower: each vote's branch waits on the VALU.)
 // A partial last segment's padding pixels are run records (copies of the pixel
 // before, interval width included), so counting them leaves "every pixel
 // exact" unchanged and spares 16 loop-invariant lane masks (SGPR spills).
@@ -1593,16 +1606,6 @@ __device__ __forceinline__ int rows_chain(IvS (&v)[S], IvS r0, IvS r1, IvS r2, c
   return go ? nlu : lu;
 }
 
-// rows_chain when every input is exact (r0..r2 and the kept pixels): plain
-// arithmetic, no intervals.  Only after the W_CUR words are resolved.
-__device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, uint32_t l3, uint32_t u,
-                                                    uint32_t wp) {
-  const uint32_t c = wp & SP_K;
-  const uint32_t va = ((((l1 + u) >> 1) & SP_K) + c) & SP_K;
-  const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
-  const uint32_t rlo = (sel + c) & SP_K;
-  return (wp & W_AVG) ? va : rlo;
-}
 template <int S>
 __device__ __forceinline__ int rows_chain_exact(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
                                                 const uint32_t (&prev)[S], int lu, bool go) {
@@ -1751,6 +1754,15 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     // ---- speculative pass
     IvS v[S];
     int lu = rows_spec<S>(v, r0, r1, r2, w, prev);
+#ifdef NICE_AB_SPEC2   // A/B probe: the speculative pass twice (its cost)
+    {
+      IvS v2[S];
+      const int lu2 = rows_spec<S>(v2, IvS{v[S - 1].lo & 1u, r0.len}, r1, r2, w, prev);
+      lu = lu2 < -1 ? lu2 : lu;
+#pragma unroll
+      for (int p = 0; p < S; ++p) v[p].lo |= v2[p].len & 0x80000000u;
+    }
+#endif
     if (active) {
       uint32_t* t = tails + lane * 6;
       t[0] = v[S - 1].lo; t[1] = v[S - 1].len;

@@ -195,7 +195,7 @@ enum {
   NICE_PH_ENC_CLASSIFY = 0, NICE_PH_ENC_TAILRUNS, NICE_PH_ENC_TABLES, NICE_PH_ENC_HEADER,
   NICE_PH_ENC_TILEBITS, NICE_PH_ENC_TILESCAN, NICE_PH_ENC_PACK, NICE_PH_ENC_TAIL, NICE_PH_ENC_LONG,
   NICE_PH_DEC_TABLES, NICE_PH_DEC_SYNC, NICE_PH_DEC_SCAN, NICE_PH_DEC_EMIT, NICE_PH_DEC_RECON,
-  NICE_PH_DEC_PLACE, NICE_PHASES
+  NICE_PH_DEC_PLACE, NICE_PH_DEC_RESYNC, NICE_PHASES   /* RESYNC: sync iterations after the first */
 };
 int nice_ctx_set_timing(nice_ctx* ctx, int on);
 /* Sums (ms) and launch counts per phase since the last read; synchronises. */
