@@ -560,14 +560,14 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // single-wave kernel otherwise
   const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
-  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;   // rows_ring_stride
-  const bool rows_in_lds = rows_thr <= 512 && rows_lds <= 160 * 1024;
+  const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;   // rows_ring_stride
+  const bool rows_in_lds = rows_thr <= 512 && rows_lds + 1024 <= 160 * 1024;   // + static LDS
   // 8-pixel segments, twice the lanes per frame, where 16-pixel segments
   // would leave SIMDs of a frame's CU idle (W <= 2048: at most two waves) and
   // frames do not share CUs: 64 x 1080p 7.83 -> 6.32 ms; slower at 4K (four
   // waves already: single frame 16.1 -> 17.7 ms).  NICE_DEC_SEG=8/16 forces a size
   const uint32_t rows8_thr = ((w + 7) / 8 + 63) / 64 * 64;
-  const size_t rows8_lds = ((size_t)rows8_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 17)) * 4;
+  const size_t rows8_lds = ((size_t)rows8_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;
   bool rows8 = use_rows && rows_in_lds && rows_thr <= 128 && rows8_thr <= 512 && rows8_lds <= 160 * 1024 &&
                n_frames <= (uint32_t)ctx->cus;
   if (const char* ev = getenv("NICE_DEC_SEG")) rows8 = atoi(ev) == 8 && use_rows && rows_in_lds &&
@@ -586,7 +586,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
   const size_t rowbuf = split ? 0
-                      : use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 17) * 4)
+                      : use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 24) * 4)
                                  : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
   // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
   // a slice with more parses its events again in dec_emit) unless the scratch

@@ -1637,9 +1637,14 @@ __device__ __forceinline__ void rows_barrier() {
   }
 }
 
-// Ring row: W pixels padded one word per 16, plus 16 spare words that take a
-// partial last segment's padding pixels (stored unmasked).
-__host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 17; }
+// Ring row: W pixels padded one word per 16 (pixel x at x + (x >> 4)), plus 16
+// spare words that take a partial last segment's padding pixels (stored
+// unmasked), and halos so that no reference needs wrap logic: words -4..-2 hold
+// the previous row's last three pixels (x = -3..-1), words g(W..W+2) the next
+// row's first three (written when that row is emitted; the spare words of the
+// previous use are overwritten by then).
+constexpr uint32_t ROWS_RB = 4;   // left halo words before pixel 0
+__host__ __device__ constexpr uint32_t rows_ring_stride(uint32_t W) { return W + (W >> 4) + 24; }
 
 template <int MAXT, bool LDS_RING, int S = ROWS_SEG>
 __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
@@ -1672,7 +1677,22 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   // ring rows padded one word per 16 pixels: lane i's segment starts at bank
   // 17i mod 32, so the lanes' accesses to their segments are conflict free
   const uint32_t RS = rows_ring_stride(W);
-  uint32_t* ring = LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * RS);
+  uint32_t* ring = (LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * RS)) + ROWS_RB;
+  // per-row class table (S == 16), double-buffered by row parity: x = kind bits
+  // | pixels back + 3, y = ring offset of the referenced row's pixel 0 plus 3
+  // minus pixels back, so a reference's word is 17 * lane + p + y (+ a +-1
+  // padding correction for the first and last three pixels of a segment)
+  __shared__ uint2 rtab[2][16];
+  auto build_tab = [&](uint32_t yy) {
+    if (threadIdx.x < 16) {
+      const uint32_t c = threadIdx.x;
+      const unsigned long long kinds = yy == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
+      const uint32_t rows = (CLS_ROWS_PACK >> (2 * c)) & 3u, dxp3 = (uint32_t)(CLS_PX_PACK >> (3 * c)) & 7u;
+      rtab[yy & 1u][c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3,
+                                    ((yy - rows) & (ROWS_RING - 1)) * RS + 3u - dxp3);
+    }
+  };
+  if (S == 16) build_tab(0);
   if (a.status[f] != 0) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t nseg = (W + S - 1) / S;
@@ -1714,10 +1734,45 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     // ---- pre-pass: records -> per-pixel words
     const uint32_t* const cwt = clsw + (y == 0 ? 16 : 0);
     uint32_t w[S];
+#ifdef NICE_AB_PRE2   // A/B probe: the pre-pass twice (its cost)
+    for (int rep = 0; rep < 2; ++rep) {
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+#else
+    {
+      constexpr uint32_t z = 0;
+#endif
+    if constexpr (S == 16) {
+      // table form: every lane, no wrap logic (ring halos); only the last
+      // lane's references to the current row (W_CUR) are patched below
+      const uint2* tb = rtab[y & 1u];
+      const uint32_t lb = 17u * lane;
+#pragma unroll
+      for (int p = 0; p < S; ++p) {
+        const uint32_t r = rec_canon(rn[p] + z, a.rec_tag);
+        const uint32_t cls = r >> 24;                        // 0..13
+        const uint2 e = tb[cls];
+        uint32_t ad = lb + e.y;
+        if (p < 3 || p > S - 4) ad += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
+        const uint32_t o = ring[ad + p];
+        const uint32_t c = spread3(r & 0xFFFFFFu);
+        w[p] = (e.x & 0xF0000000u) | (((cls >= 4u ? o : 0u) + c) & SP_K);
+      }
+      if (lane == nseg - 1) {   // references past the row end into row y itself: pixels 0..2
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          const uint32_t r = rec_canon(rn[p], a.rec_tag);
+          const uint32_t cls = r >> 24;
+          const uint32_t tx = x0 + p + 3u - (tb[cls].x & 7u);
+          if (cls >= 4u && ((CLS_ROWS_PACK >> (2 * cls)) & 3u) == 1u && tx >= W && p < nvalid)
+            w[p] = W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8);
+        }
+      }
+    } else {
 #pragma unroll
     for (int p = 0; p < S; ++p) {
       const uint32_t x = x0 + p;
-      const uint32_t r = rec_canon(rn[p], a.rec_tag);
+      const uint32_t r = rec_canon(rn[p] + z, a.rec_tag);
       const uint32_t cls = r >> 24;                          // 0..13
       const uint32_t cw = cwt[cls];                          // rows | px + 3 << 2 | kind bits
       const uint32_t rows = cw & 3u;
@@ -1736,6 +1791,8 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       // nested exec-masked branches per pixel)
       const uint32_t kb = (cw & 0xF0000000u) | (cur ? W_CUR : 0u);
       w[p] = kb | ((up && !cur) ? ((o + c) & SP_K) : c) | (cur ? ((uint32_t)tx << 8) : 0u);
+    }
+    }
     }
     // ---- entry: lane 0 exact (previous row's last pixels; 0 before pixel 0)
     IvS r0{0u, SP_K}, r1{0u, SP_K}, r2{0u, SP_K};
@@ -1780,6 +1837,12 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     rows_barrier<LDS_RING>();
     const unsigned long long c2 = stats ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long nfix0 = n_fix;
+#ifdef NICE_AB_ROUND   // A/B probe: one more (empty) fix-up round per row
+    if (!fin) atomicOr(&pend[1], 0u);
+    rows_barrier<LDS_RING>();
+    if (pend[1] == 7u) lu = S;
+    rows_barrier<LDS_RING>();
+#endif
     // ---- fix-up rounds
     bool cur_done = false;
     for (uint32_t rd = 0;; ++rd) {
@@ -1830,6 +1893,17 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const uint64_t pix = (uint64_t)y * W + x0;
 #pragma unroll
       for (int p = 0; p < S; ++p) rr[p] = v[p].lo;   // padding pixels land in the row's spare words
+      if (lane == 0 && y > 0) {   // row y-1's right halo: this row's first three pixels
+        uint32_t* h = ring + (size_t)((y - 1) & (ROWS_RING - 1)) * RS;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) h[(W + k) + ((W + k) >> 4)] = v[k].lo;
+      }
+      if (lane == nseg - 1) {     // row y+1's left halo: this row's last three pixels
+        uint32_t* h = ring + (size_t)((y + 1) & (ROWS_RING - 1)) * RS;
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+          if (p < nvalid && x0 + p + 3u >= W) h[(int)(x0 + p - W) - 1] = v[p].lo;
+      }
       if (vec_out && OC == 4) {
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
 #pragma unroll
@@ -1869,6 +1943,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     }
 #pragma unroll
     for (int p = 0; p < S; ++p) { prev[p] = v[p].lo; }
+    if (S == 16) build_tab(y + 1);   // the last readers of that buffer were row y-1's
     rows_barrier<LDS_RING>();
     if (stats) {
       const unsigned long long c4 = __builtin_amdgcn_s_memtime();
