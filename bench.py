@@ -570,7 +570,7 @@ def main():
     out_px_bytes = F * N * 4
     algo = {
         "enc_classify": in_bytes, "enc_pack": stream_bytes,
-        "dec_sync": stream_bytes, "dec_emit": stream_bytes,
+        "dec_sync": stream_bytes, "dec_resync": stream_bytes, "dec_emit": stream_bytes,
         "dec_reconstruct": out_px_bytes,
     }
     dom = max((k for k in phase if k in algo), key=lambda k: phase[k]["ms_total"])
