@@ -1557,17 +1557,9 @@ __device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, ui
                                                     uint32_t wp) {
   const uint32_t c = wp & SP_K;
   const uint32_t va = ((((l1 + u) >> 1) & SP_K) + c) & SP_K;
-#ifdef NICE_AB_EXACT_SEL
   const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
   const uint32_t rlo = (sel + c) & SP_K;
   return (wp & W_AVG) ? va : rlo;
-#else
-  // kinds by masks, as rows_step (the select chain compiled to compares and
-  // dependent selects)
-  const uint32_t sel = (l1 & wmask(wp, 28)) | (l2 & wmask(wp, 29)) | (l3 & wmask(wp, 30));
-  const uint32_t ma = wmask(wp, 31);
-  return (va & ma) | (((sel + c) & SP_K) & ~ma);
-#endif
 }
 
 // Speculative pass over the whole segment; returns the last unknown index.
@@ -1619,11 +1611,9 @@ __device__ __forceinline__ int rows_chain_exact(IvS (&v)[S], IvS r0, IvS r1, IvS
                                                 const uint32_t (&prev)[S], int lu, bool go) {
   const int upto = go ? lu : -1;
   // all S steps, predicated: a vote per pixel to stop early (its branch waits
-  // on the VALU) made a single 4K frame 4 % slower, same at 512 frames; one
-  // vote per call skips waves with nothing to recompute
-#ifndef NICE_AB_CHAIN_NOSKIP
-  if (!__any(go)) return lu;
-#endif
+  // on the VALU) made a single 4K frame 4 % slower, same at 512 frames (one
+  // vote per call to skip waves with nothing to recompute, and kind masks
+  // instead of the select chain, were no faster either)
 #pragma unroll
   for (int p = 0; p < S; ++p) {
     const uint32_t l1 = p >= 1 ? v[p - 1].lo : r0.lo;
