@@ -151,7 +151,7 @@ def load_traffic(phase, frames, path=None):
     summary (bytes per frame from separate FETCH_SIZE / WRITE_SIZE passes,
     gfx950-corrected; see profiles/README.md), scaled to this launch's frame
     count; None if absent."""
-    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r03c.json")
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r03d.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
