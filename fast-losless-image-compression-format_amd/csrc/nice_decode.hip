@@ -1562,7 +1562,8 @@ __device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, ui
   return (wp & W_AVG) ? va : rlo;
 }
 
-// Speculative pass over the whole segment; returns the last unknown index.
+// Speculative pass over the whole segment; returns -1 when every pixel is
+// exact, S - 4 when the last three are, else S - 1 (a bound on the last unknown).
 // (Switching a wave to the plain step once all its lanes are exact -- one
 // vote per pixel -- was 5 % slower: each vote's branch waits on the VALU.)
 // A partial last segment's padding pixels are run records (copies of the pixel
@@ -1571,16 +1572,21 @@ __device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, ui
 template <int S>
 __device__ __forceinline__ int rows_spec(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
                                          const uint32_t (&prev)[S]) {
-  int lu = -1;
 #pragma unroll
   for (int p = 0; p < S; ++p) {
     const IvS l1 = p >= 1 ? v[p - 1] : r0;
     const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
     const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
     v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
-    lu = v[p].len ? p : lu;
   }
-  return lu;
+  // a coarse last unknown index from two OR trees instead of a compare and a
+  // select per pixel: its users only ask "any unknown" and "last three exact",
+  // and the fix-up chain recomputing exact pixels too is harmless (512-frame
+  // reconstruct 20.03 -> 19.63 ms)
+  uint32_t head = 0, tail = v[S - 1].len | v[S - 2].len | v[S - 3].len;
+#pragma unroll
+  for (int p = 0; p < S - 3; ++p) head |= v[p].len;
+  return tail ? S - 1 : head ? S - 4 : -1;
 }
 
 // Recomputes pixels 0..lu (lanes with `go`), keeping the others (already
