@@ -144,7 +144,8 @@ struct BandState {
   bool classified = false, tabled = false;
   nice::EncArgs a{};
   uint64_t band_bits = 0, seed_bit = 0;
-  uint32_t* bhist = nullptr;   // the band's own symbol counts (nice_band_runs), for its bit count
+  uint32_t* bhist = nullptr;
+  const unsigned long long* d_info = nullptr;   // nice_band_tables_dev's output (checked by the pack)   // the band's own symbol counts (nice_band_runs), for its bit count
 };
 
 struct nice_ctx {
@@ -158,6 +159,9 @@ struct nice_ctx {
   uint64_t rec_words = 0, rec_gen = 0;
   uint32_t rec_epoch = 0;
   int cus = 0;   // compute units of the device (enc_pack's persistent grid)
+  // the last split decode's per-frame abort flags (test hook nice_test_split_redos)
+  const uint32_t* split_abort = nullptr;
+  uint32_t split_frames = 0;
 };
 
 extern "C" {
@@ -273,6 +277,11 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.px_lo = 0;
   a.px_hi = (int64_t)N;
   a.band = 0;
+  a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * 32;
+  if (const char* ev = getenv("NICE_ENC_PACK_CAP")) {   // tests: bits per pixel of the LDS buffer
+    const int b = atoi(ev);
+    if (b >= 1 && b <= 32) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * (uint32_t)b;
+  }
   return a;
 }
 }  // namespace
@@ -526,6 +535,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   if (N > 0 && (!d_px || px_stride < N * out_channels)) return NICE_E_ARG;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
+  ctx->split_frames = 0;
   NICE_HIP(hipMemsetAsync(d_status, 0, (size_t)n_frames * 4, st));
   // stream lengths bound the chunk grid
   std::vector<uint64_t> lens(n_frames);
@@ -559,7 +569,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // multi-wave row kernel for 64 <= W <= 16384 (one lane per 16-pixel segment),
   // single-wave kernel otherwise
   const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
-  const bool use_rows = w >= 64 && rows_thr <= 1024 && !getenv("NICE_DEC_SINGLE_WAVE");
+  const bool single_wave = getenv("NICE_DEC_SINGLE_WAVE") != nullptr;
+  const bool use_rows = w >= 64 && rows_thr <= 1024 && !single_wave;
   const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds + 1024 <= 160 * 1024;   // + static LDS
   // 8-pixel segments, twice the lanes per frame, where 16-pixel segments
@@ -573,21 +584,32 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   if (const char* ev = getenv("NICE_DEC_SEG")) rows8 = atoi(ev) == 8 && use_rows && rows_in_lds &&
                                                        rows8_thr <= 512 && rows8_lds <= 160 * 1024;
   // wide frames, few of them: strips of <= 256 segments on separate CUs
-  // (dec_rows_split; every block must be resident: at most one per CU for
-  // half the CUs); NICE_DEC_SPLIT=k forces k strips (tests), =0 disables
+  // (dec_rows_split; its blocks wait on each other, so they should all be
+  // resident: at most one per CU for half the CUs, frames in chunks of that
+  // many strips).  When they are not (other kernels hold the CUs), a strip's
+  // wait times out and the frame goes to the fallback launch (dec_rows_wide,
+  // or dec_reconstruct above 16384 columns) -- slower, never wrong.
+  // NICE_DEC_SPLIT=k forces k strips (tests), =0 disables
   const uint32_t nseg16 = (w + 15) / 16;
-  uint32_t strips = use_rows ? (nseg16 + SPLIT_THREADS_HOST - 1) / SPLIT_THREADS_HOST : 1;
+  const uint32_t split_cap = (uint32_t)std::max(ctx->cus / 2, 1);
+  uint32_t strips = (nseg16 + SPLIT_THREADS_HOST - 1) / SPLIT_THREADS_HOST;
   if (const char* ev = getenv("NICE_DEC_SPLIT")) strips = (uint32_t)atoi(ev);
-  bool split = use_rows && strips >= 2 && (uint64_t)n_frames * strips <= (uint64_t)std::max(ctx->cus / 2, 1);
+  // <= 16384 columns: only when the whole batch fits at once (else one block
+  // per frame is the better use of the CUs); wider: always, in frame chunks
+  bool split = !single_wave && w >= 64 && strips >= 2 && strips <= split_cap &&
+               (!use_rows || (uint64_t)n_frames * strips <= split_cap);
   if (split) {
     const uint32_t sps = (nseg16 + strips - 1) / strips;
     // every strip >= 2 segments (>= 3 pixels: its first and last three) and <= 256 lanes
     if (sps > SPLIT_THREADS_HOST || nseg16 <= (strips - 1) * sps + 1) split = false;
   }
+  const uint32_t split_frames = split ? std::min(n_frames, split_cap / strips) : 0;   // frames per launch
   const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
-  const size_t rowbuf = split ? 0
-                      : use_rows ? (rows_in_lds ? 0 : (size_t)n_frames * 4 * (w + (w >> 4) + 24) * 4)
-                                 : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
+  // the row ring in global memory: dec_rows_wide (also the split path's
+  // fallback) or dec_reconstruct without room in LDS
+  const size_t ring_rows = use_rows ? (size_t)n_frames * 4 * (w + (w >> 4) + 24) * 4
+                                    : (g.in_lds ? 0 : (size_t)n_frames * g.R * w * 4);
+  const size_t rowbuf = split ? ring_rows : (use_rows && rows_in_lds) ? 0 : ring_rows;
   // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
   // a slice with more parses its events again in dec_emit) unless the scratch
   // does not fit, then every slice is parsed again in dec_emit
@@ -741,7 +763,22 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     size_t lds = ((size_t)SPLIT_THREADS_HOST * 7 + 4 + 4 * ((size_t)sps * 16 + 6 + ((sps * 16 + 6) >> 4) + 17)) * 4;
     lds = std::max<size_t>(lds, 82 * 1024);
     NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(dec_rows_split, dim3(n_frames * strips), dim3(SPLIT_THREADS_HOST), lds, st, a);
+    for (uint32_t f0 = 0; f0 < n_frames; f0 += split_frames) {
+      a.split_f0 = f0;
+      hipLaunchKernelGGL(dec_rows_split, dim3(std::min(split_frames, n_frames - f0) * strips),
+                         dim3(SPLIT_THREADS_HOST), lds, st, a);
+    }
+    a.split_f0 = 0;
+    // fallback: frames whose strips timed out waiting for a non-resident
+    // neighbour (every other block returns at once)
+    DecArgs r = a;
+    r.redo = 1;
+    if (use_rows)
+      hipLaunchKernelGGL(dec_rows_wide, dim3(n_frames), dim3(rows_thr), ((size_t)rows_thr * 7 + 8) * 4, st, r);
+    else
+      hipLaunchKernelGGL(dec_reconstruct, dim3(n_frames), dim3(64), g.lds, st, r);
+    ctx->split_abort = a.hand_abort;
+    ctx->split_frames = n_frames;
   } else if (use_rows && rows_in_lds && rows8) {
     if (rows8_lds > 64 * 1024)
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows8, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -922,6 +959,7 @@ int nice_band_tables_dev(nice_ctx* ctx, void* stream, const uint32_t* d_hist_tot
   ctx->bs.tabled = true;
   ctx->bs.band_bits = ~0ull;   // known to the caller once d_info is read (nice_band_pack_bits)
   ctx->bs.seed_bit = ~0ull;
+  ctx->bs.d_info = (const unsigned long long*)d_info;
   return NICE_OK;
 }
 
@@ -959,6 +997,8 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;
   NICE_HIP(hipMemsetAsync(a.status, 0, (size_t)ng * 8, st));
   NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
+  if (ctx->bs.d_info)   // the bit count the caller read back must be the device's
+    hipLaunchKernelGGL(enc_band_check, dim3(1), dim3(64), 0, st, a, ctx->bs.d_info, (unsigned long long)band_bits);
   // FLAG_LONG (the launches return at once otherwise): tile bits, their scan from
   // band_bit0, the codes that fit the cache, then the wrapped writes
   const uint32_t tblocks = std::min<uint32_t>(nt, 2048u);
@@ -1079,6 +1119,43 @@ int nice_test_code_lengths(const uint32_t* counts, int n_vec, int n, uint8_t* ao
   (void)hipFree(dc);
   (void)hipFree(da);
   return rc;
+}
+
+// Test hooks for dec_rows_split's fallback (tests/test_split.py).
+// nice_test_occupy: `blocks` blocks of `lds_bytes` dynamic LDS each (one per
+// CU at > 80 KB) on `stream`; blocks < short_blocks spin short_us, the others
+// long_us (bounded busy waits on the real-time counter).
+__global__ void nice_occupy_kernel(uint32_t short_blocks, unsigned long long short_ticks,
+                                   unsigned long long long_ticks) {
+  extern __shared__ uint32_t occ_lds[];
+  if (threadIdx.x == 0) occ_lds[0] = blockIdx.x;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long d = blockIdx.x < short_blocks ? short_ticks : long_ticks;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(127);
+}
+int nice_test_occupy(void* stream, uint32_t blocks, uint32_t short_blocks, uint32_t short_us, uint32_t long_us,
+                     uint32_t lds_bytes) {
+  if (blocks == 0 || lds_bytes > 160 * 1024 || long_us > 5000000 || short_us > 5000000) return NICE_E_ARG;
+  NICE_HIP(hipFuncSetAttribute((const void*)nice_occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds_bytes));
+  hipLaunchKernelGGL(nice_occupy_kernel, dim3(blocks), dim3(64), lds_bytes, (hipStream_t)stream, short_blocks,
+                     (unsigned long long)short_us * 100ull, (unsigned long long)long_us * 100ull);
+  NICE_HIP(hipGetLastError());
+  return NICE_OK;
+}
+// Frames of the context's last split decode that went to the fallback launch
+// (synchronises the device).
+int nice_test_split_redos(nice_ctx* ctx, uint32_t* split_frames, uint32_t* redos) {
+  if (!ctx || !redos || !split_frames) return NICE_E_ARG;
+  *redos = 0;
+  *split_frames = ctx->split_frames;
+  if (!ctx->split_abort || !ctx->split_frames) return NICE_OK;
+  NICE_HIP(hipSetDevice(ctx->device));
+  NICE_HIP(hipDeviceSynchronize());
+  std::vector<uint32_t> h(ctx->split_frames);
+  NICE_HIP(hipMemcpy(h.data(), ctx->split_abort, h.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t v : h) *redos += v == SPLIT_REDO ? 1u : 0u;
+  return NICE_OK;
 }
 
 const char* nice_phase_name(int phase) {

@@ -1398,6 +1398,7 @@ __device__ __forceinline__ void dec_reconstruct_body(const DecArgs& a) {
   else ring = a.rowbuf + (uint64_t)blockIdx.x * R * W;
   const uint32_t f = blockIdx.x;
   const int lane = threadIdx.x;
+  if (a.redo && a.hand_abort[f] != SPLIT_REDO) return;
   if (a.status[f] != 0) return;
   if (lane < 16) {
     L.ref_k[lane] = cls_rows(lane);
@@ -1702,6 +1703,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     }
   };
   if (S == 16) build_tab(0);
+  if (a.redo && a.hand_abort[f] != SPLIT_REDO) return;   // block-uniform
   if (a.status[f] != 0) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t nseg = (W + S - 1) / S;
@@ -2000,7 +2002,11 @@ __global__ __launch_bounds__(512) void dec_rows8(DecArgs a) { dec_rows_body<512,
 // on an error).
 // ---------------------------------------------------------------------------
 constexpr uint32_t SPLIT_THREADS = 256;                      // lanes (16-pixel segments) per strip
-constexpr unsigned long long SPLIT_TIMEOUT = 400000000ull;   // s_memrealtime ticks (100 MHz): 4 s
+// s_memrealtime ticks (100 MHz): 0.2 s.  A wait this long means a strip's
+// neighbour is not resident (other kernels hold the CUs): the frame is handed
+// to the fallback launch (SPLIT_REDO), not failed
+constexpr unsigned long long SPLIT_TIMEOUT = 20000000ull;
+constexpr int SPLIT_QUIET = -1000, SPLIT_TIMED_OUT = -1001;   // block-local err codes
 constexpr uint32_t SPLIT_GRAN = 8;                           // granules per unit: first3 at 0..2, last3 at 4..6
 __host__ __device__ constexpr uint32_t split_ring_stride(uint32_t sw) { return (sw + 6) + ((sw + 6) >> 4) + 17; }
 __device__ __forceinline__ uint32_t sr_idx(uint32_t lc3) { return lc3 + (lc3 >> 4); }
@@ -2099,7 +2105,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
   __shared__ uint32_t pend[2];
   __shared__ int err;
   const uint32_t k = a.strips;
-  const uint32_t f = blockIdx.x / k, j = blockIdx.x % k;
+  const uint32_t f = a.split_f0 + blockIdx.x / k, j = blockIdx.x % k;
   const uint32_t W = a.W, H = a.H;
   const uint32_t nseg = (W + S - 1) / S;
   const uint32_t sps = (nseg + k - 1) / k;
@@ -2157,11 +2163,11 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
   // wave 0: gives up (error) on a timeout or another strip's abort
   auto give_up = [&]() -> bool {
     if (__hip_atomic_load(abort_f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-      if (lane == 0) atomicCAS(&err, 0, -1000);   // another strip failed: exit quietly
+      if (lane == 0) atomicCAS(&err, 0, SPLIT_QUIET);   // another strip failed or timed out: exit quietly
       return true;
     }
     if (__builtin_amdgcn_s_memrealtime() - t_row > SPLIT_TIMEOUT) {
-      if (lane == 0) atomicCAS(&err, 0, NICE_E_HIP);
+      if (lane == 0) atomicCAS(&err, 0, SPLIT_TIMED_OUT);
       return true;
     }
     return false;
@@ -2421,8 +2427,12 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
     atomicAdd(&stats[3], c_entry); atomicAdd(&stats[9], c_right);
   }
   if (lane == 0 && err) {
-    if (err != -1000) {
-      __hip_atomic_store(abort_f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (err == SPLIT_TIMED_OUT) {
+      // not co-resident: the fallback launch reconstructs the frame (a real
+      // error of another strip sets the status, which the fallback respects)
+      atomicCAS(abort_f, 0u, SPLIT_REDO);
+    } else if (err != SPLIT_QUIET) {
+      __hip_atomic_store(abort_f, SPLIT_ABORT_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       set_status(&a.status[f], err);
     }
   }

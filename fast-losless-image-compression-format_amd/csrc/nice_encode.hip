@@ -1533,7 +1533,7 @@ __device__ __forceinline__ void tile_range(const EncArgs& a, uint64_t& w0, uint6
 
 // frames the long-code path handles: all (bands), or those with FLAG_LONG
 __device__ __forceinline__ bool long_path(const EncArgs& a, uint32_t f) {
-  return !a.long_only || (a.frame_flags[f] & FLAG_LONG);
+  return (!a.long_only || (a.frame_flags[f] & FLAG_LONG)) && !(a.frame_flags[f] & FLAG_BAD);
 }
 
 __global__ __launch_bounds__(ENC_THREADS) void enc_tilebits(EncArgs a) {
@@ -1759,13 +1759,13 @@ __device__ void pack_next(const EncArgs& a, uint32_t nt, uint32_t I, uint32_t sl
     const uint32_t own = slot + seq * I;
     if (own < F) {
       ++seq;
-      f = (a.frame_flags[own] & FLAG_LONG) ? NONE : own;   // long frames: enc_pack_long
+      f = (a.frame_flags[own] & (FLAG_LONG | FLAG_BAD)) ? NONE : own;   // long frames: enc_pack_long
       continue;
     }
     f = NONE;
     for (uint32_t b0 = 0; b0 < F; b0 += 64) {
       const uint32_t g = b0 + (uint32_t)lane;
-      const bool cand = g < F && !(a.frame_flags[g] & FLAG_LONG) &&
+      const bool cand = g < F && !(a.frame_flags[g] & (FLAG_LONG | FLAG_BAD)) &&
                         __hip_atomic_load(&a.pack_ctr[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nt;
       const unsigned long long m = __ballot(cand);
       if (m) { f = b0 + (uint32_t)__builtin_ctzll(m); break; }
@@ -1941,7 +1941,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
         sbits += ws;
       }
       PROF_MARK(1);
-      over = over || gbits + sbits > (uint32_t)PACK_CAP_BITS;
+      over = over || gbits + sbits > a.pack_cap_bits;
       if (!over && C.nb) {
         // at bit pp, MSB-first: one 64-bit shift places the bits across
         // words pp >> 5 and pp >> 5 + 1, both OR-ed into LDS (words shared
@@ -2046,7 +2046,9 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
       if (!over && !(nw && sh)) a.tile_bits[t0] = 0u;
       if (tt0 + nsub == T) a.data_end[f] = e0;
     }
-    used_words = over ? 0u : nw + 1;
+    // an over-cap group has OR-ed its first tiles into the buffer before it
+    // went over: the next group clears all of it
+    used_words = over ? (uint32_t)PACK_MAX_WORDS : nw + 1;
     PROF_MARK(4);
     // the next group: claimed only now, when this block can start it at once
     // (a group claimed earlier would keep the look-backs of the groups after
@@ -2077,7 +2079,7 @@ __global__ __launch_bounds__(256) void enc_edges(EncArgs a) {
   const uint32_t T = a.tiles_per_frame;
   const uint32_t ng = (a.tile_hi - a.tile_lo + PACK_SUB - 1) / PACK_SUB;   // groups of the frame (band)
   for (uint32_t f = blockIdx.y; f < a.n_frames; f += gridDim.y) {
-    if (a.frame_flags[f] & FLAG_LONG) continue;
+    if (a.frame_flags[f] & (FLAG_LONG | FLAG_BAD)) continue;
     uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
     for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < ng; g += gridDim.x * 256) {
       const uint64_t t = (uint64_t)f * T + a.tile_lo + (uint64_t)g * PACK_SUB;
@@ -2154,7 +2156,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
   TileIter it(a, t0);
   for (uint64_t w = t0; w < t1; ++w, it.step(1)) {
     const uint32_t f = it.f, tt = it.tt();
-    if (!(a.frame_flags[f] & FLAG_LONG)) continue;   // block-uniform
+    if ((a.frame_flags[f] & (FLAG_LONG | FLAG_BAD)) != FLAG_LONG) continue;   // block-uniform
     const uint64_t t = it.tile();
     const int64_t start = (int64_t)tt * ENC_TILE;
     const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
@@ -2314,6 +2316,14 @@ __global__ __launch_bounds__(256) void enc_band_edges(EncArgs a, uint32_t* edges
 // The band's data bits: its own symbol counts (bhist, 858 bins; the mode
 // prefixes derived from the payload streams as enc_tables does) times the code
 // lengths of the shared tables.  info = {bits, data start bit}.
+// nice_band_pack_bits after nice_band_tables_dev: the band_bits argument must
+// be the device count (d_info[0]); on a mismatch the band is flagged FLAG_BAD
+// and the pack kernels write nothing (the flag is recomputed on every call)
+__global__ void enc_band_check(EncArgs a, const unsigned long long* info, unsigned long long band_bits) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    a.frame_flags[0] = (a.frame_flags[0] & ~FLAG_BAD) | (info[0] != band_bits ? FLAG_BAD : 0u);
+}
+
 __global__ __launch_bounds__(256) void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info) {
   __shared__ unsigned long long s_bits;
   __shared__ uint32_t s_mode[5];

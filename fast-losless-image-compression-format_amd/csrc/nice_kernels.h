@@ -10,6 +10,10 @@ constexpr int ENC_TILE = 1024;          // pixels per encoder tile (raster-conti
 // frame emits a code longer than FAST_MAX_CODE_BITS: packed by enc_pack_long
 // (the reference writer's u32 cache wraps for such codes, bitwriter.rs:63-64)
 constexpr uint32_t FLAG_LONG = 1u;
+// band pack: the caller's band_bits differ from the band's real bit count
+// (nice_band_pack_bits after nice_band_tables_dev): the pack kernels skip the
+// band instead of writing past the caller's words
+constexpr uint32_t FLAG_BAD = 2u;
 
 struct EncArgs {
   // input: n_frames frames of W*H pixels, C bytes per pixel, frame_stride bytes apart
@@ -66,6 +70,10 @@ struct EncArgs {
   // aggregate (n_frames * groups: min first coded pixel, then bit total)
   uint32_t groups;
   unsigned long long* gacc;
+  // enc_pack: bits a group may hold in its LDS buffer (PACK_SUB * ENC_TILE * 32;
+  // NICE_ENC_PACK_CAP=b lowers it to b bits per pixel, so tests reach the
+  // over-cap path on ordinary frames)
+  uint32_t pack_cap_bits;
 };
 constexpr uint32_t ENC_GROUP_TILES = 8192;
 
@@ -97,6 +105,7 @@ constexpr int PACK_SUB = 4;                  // tiles per enc_pack work item (gr
 __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
 __global__ void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info);
+__global__ void enc_band_check(EncArgs a, const unsigned long long* info, unsigned long long band_bits);
 __global__ void enc_band_fix(uint8_t* out, const uint32_t* words, const unsigned long long* band_bit0,
                              const unsigned long long* band_off, uint32_t R);
 __global__ void enc_band_merge(uint32_t* out32, const uint32_t* words, const unsigned long long* band_w0,
@@ -161,7 +170,13 @@ struct DecArgs {
   uint32_t strips;
   unsigned long long* hand;
   uint32_t* hand_abort;
+  uint32_t split_f0;                  // dec_rows_split: first frame of this launch (frames in chunks)
+  // the fallback launch after dec_rows_split (dec_rows_wide / dec_reconstruct):
+  // only frames whose strips could not all be resident (hand_abort ==
+  // SPLIT_REDO: a wait timed out) are reconstructed, the others return at once
+  uint32_t redo;
 };
+constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
 // EV_RUN | pixels (saturated)
 constexpr uint32_t EV_RUN = 1u << 31, EV_BAD = 1u << 29, EV_L2 = 1u << 28;

@@ -127,7 +127,11 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
  *   nice_band_runs_dev      band_next read from device memory (u32)
  *   nice_band_tables_dev    d_info[0] = the band's data bits, d_info[1] = the
  *                           data start bit (device u64 x 2, written in stream order)
- *   nice_band_pack_bits     the band's bits passed in (from the gathered d_info)
+ *   nice_band_pack_bits     the band's bits passed in (from the gathered d_info);
+ *                           band_bits must equal d_info[0] exactly (it sizes the
+ *                           band's words): after nice_band_tables_dev the device
+ *                           compares them and, on a mismatch, writes no band bits
+ *                           (d_words is then undefined, never overrun)
  * nice_band_assemble after nice_band_tables_dev takes band_bit0[0] as the data
  * start.
  * d_px holds pixels [px0, px0 + px_count) (global raster index), which must

@@ -302,9 +302,13 @@ static inline int rgb_eq(const uint8_t *in, size_t a, size_t b) {
     return in[a] == in[b] && in[a + 1] == in[b + 1] && in[a + 2] == in[b + 2];
 }
 
-int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+/* px_bit (optional, W*H + 1 entries): the absolute stream bit of each coded
+ * pixel's first symbol, UINT64_MAX for run members, then the data end bit
+ * (test data for the band exchange rehearsal: a band's bits start at its
+ * first coded pixel's). */
+static int encode_impl(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
                        uint8_t channels, uint8_t channels_out,
-                       uint8_t **out, size_t *out_len, nice_oracle_stats *stats) {
+                       uint8_t **out, size_t *out_len, nice_oracle_stats *stats, uint64_t *px_bit) {
     *out = NULL; *out_len = 0;
     if (channels < 3) return NICE_ORACLE_E_ARG;
     const size_t W = width, ch = channels;
@@ -329,7 +333,14 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
 
     size_t position = 0, prev_position = 0;
     uint64_t n_coded = 0, n_br = 0, n_sd = 0, n_l2 = 0, n_luma = 0, n_rgb = 0, n_runpx = 0;
+    uint64_t *cp_sym = NULL;   /* px_bit: first symbol index of each coded pixel (by pixel) */
+    if (px_bit) {
+        cp_sym = (uint64_t *)malloc(8 * ((size_t)height * W + 1));
+        for (size_t i = 0; i < (size_t)height * W; ++i) { cp_sym[i] = UINT64_MAX; px_bit[i] = UINT64_MAX; }
+        cp_sym[(size_t)height * W] = UINT64_MAX;
+    }
     while (position < image_size) {                                      /* code.rs:159 */
+        if (cp_sym) cp_sym[position / ch] = e.len;
         n_coded++;
         int done = 0;
         /* back references: code.rs:191-206 */
@@ -449,8 +460,13 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
     size_t header_bytes = sink.len;
     uint8_t max_emit = 0;
     uint64_t n_long = 0, n_wrapped = 0;
+    size_t cpi = 0;   /* px_bit: next coded pixel */
     for (size_t k = 0; k < e.len; ++k) {                                /* hfe.rs:110-113 */
         int s = e.v[k].stream, sym = e.v[k].sym;
+        if (cp_sym) {
+            while (cpi < (size_t)height * W && (cp_sym[cpi] == UINT64_MAX || cp_sym[cpi] < k)) ++cpi;
+            if (cpi < (size_t)height * W && cp_sym[cpi] == k) px_bit[cpi] = 8ull * sink.len + bw.bit_offset;
+        }
         if (aob[s][sym] > max_emit) max_emit = aob[s][sym];
         /* diagnostics: codes over 25 bits, and writes whose u8 `32 - bit_offset`
          * wraps (bitwriter.rs:63-64: pending + length > 32 mangles the cache) */
@@ -458,6 +474,7 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
         n_wrapped += (unsigned)bw.bit_offset + aob[s][sym] > 32u;
         bw_write_24bits(&bw, aob[s][sym], (uint32_t)code[s][sym]);
     }
+    if (px_bit) px_bit[(size_t)height * W] = 8ull * sink.len + bw.bit_offset;   /* the data end */
     sink_put(&sink, (uint8_t)(bw.cache >> 24));                           /* hfe.rs:115 */
     for (int s = 24; s >= 0; s -= 8) sink_put(&sink, (uint8_t)(bw.cache >> s)); /* code.rs:421-422 */
 
@@ -479,12 +496,24 @@ int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_
             }
     }
     int oom = sink.oom || e.oom;
+    free(cp_sym);
     for (int s = 0; s < N_STREAMS; ++s) { free(aob[s]); free(code[s]); free(e.occ[s]); }
     free(e.v);
     if (oom) { free(sink.p); return NICE_ORACLE_E_OOM; }
     *out = sink.p;
     *out_len = sink.len;
     return 0;
+}
+
+int nice_oracle_encode(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+                       uint8_t channels, uint8_t channels_out,
+                       uint8_t **out, size_t *out_len, nice_oracle_stats *stats) {
+    return encode_impl(in, in_len, width, height, channels, channels_out, out, out_len, stats, NULL);
+}
+
+int nice_oracle_encode_bitpos(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+                              uint8_t channels, uint8_t **out, size_t *out_len, uint64_t *px_bit) {
+    return encode_impl(in, in_len, width, height, channels, channels, out, out_len, NULL, px_bit);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -998,7 +1027,7 @@ static int deep_try(uint8_t *px, size_t i, uint32_t W, uint32_t C, const int pre
 /* force (ascending pixel indices): those pixels take the rarest delta still
  * available, so the rarest (longest-code) symbols land there. */
 static void gen_deep(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
-                     const uint64_t *force, size_t n_force) {
+                     const uint64_t *force, size_t n_force, uint32_t flat_y0, uint32_t flat_y1) {
     if (K > 40) K = 40;
     if (K < 2) K = 2;
     int dl[40][3];
@@ -1022,6 +1051,10 @@ static void gen_deep(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t s
         uint8_t *p = px + i * C;
         if (C == 4) p[3] = 255;
         if (i == 0) { p[0] = 128; p[1] = 128; p[2] = 128; continue; }
+        if (i / W >= flat_y0 && i / W < flat_y1) {   /* one flat colour: a single run, no draws */
+            p[0] = 17; p[1] = 99; p[2] = 201;
+            continue;
+        }
         int pred[3];
         const uint8_t *L = px + (i - 1) * C;
         for (int c = 0; c < 3; ++c)
@@ -1047,12 +1080,51 @@ static void gen_deep(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t s
 }
 
 void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K) {
-    gen_deep(px, W, H, C, seed, K, NULL, 0);
+    gen_deep(px, W, H, C, seed, K, NULL, 0, 0, 0);
 }
 
 void nice_oracle_gen_deep_codes_at(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
                                    const uint64_t *force, size_t n_force) {
-    gen_deep(px, W, H, C, seed, K, force, n_force);
+    gen_deep(px, W, H, C, seed, K, force, n_force, 0, 0);
+}
+
+/* as gen_deep_codes_at, with rows [flat_y0, flat_y1) one flat colour (a run
+ * that consumes no draws, so the Fibonacci counts stay intact) */
+void nice_oracle_gen_deep_codes_flat(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
+                                     const uint64_t *force, size_t n_force, uint32_t flat_y0, uint32_t flat_y1) {
+    gen_deep(px, W, H, C, seed, K, force, n_force, flat_y0, flat_y1);
+}
+
+/* A frame of RGB-mode pixels (code.rs:341-366) whose residuals against the
+ * prediction floor((U+L)/2) (L in row 0) take 11 values per channel with
+ * geometric weights 2^-(k+1), except rows noise[0..n_noise) which are uniform
+ * noise.  The Huffman tree of stream 0 is then a chain, so the noise rows'
+ * residuals get long (but <= 25-bit) codes: over 32 bits per pixel
+ * (enc_pack's over-cap path at the real cap). */
+void nice_oracle_gen_rgb_field(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed,
+                               const uint32_t *noise, size_t n_noise) {
+    uint32_t s = seed ? seed : 1u;
+#define XS() (s ^= s << 13, s ^= s >> 17, s ^= s << 5, s)
+    const size_t N = (size_t)W * H;
+    size_t ni = 0;
+    for (size_t i = 0; i < N; ++i) {
+        uint8_t *p = px + i * C;
+        if (C == 4) p[3] = 255;
+        const uint32_t y = (uint32_t)(i / W);
+        while (ni < n_noise && noise[ni] < y) ++ni;
+        const int is_noise = ni < n_noise && noise[ni] == y;
+        const uint32_t r = XS();
+        for (int c = 0; c < 3; ++c) {
+            int pred = 0;
+            if (i >= W) pred = ((int)px[(i - W) * C + c] + (int)px[(i - 1) * C + c]) / 2;
+            else if (i > 0) pred = px[(i - 1) * C + c];
+            /* geometric residual: value k (P = 2^-(k+1), k < 11) per channel */
+            const uint32_t bits = (r >> (10 * c)) & 0x3FFu;
+            const int k = bits ? __builtin_ctz(bits) : 10;
+            p[c] = is_noise ? (uint8_t)(r >> (8 * c)) : (uint8_t)(pred + 40 + 13 * k);
+        }
+    }
+#undef XS
 }
 
 /* ------------------------------------------------------------------------- */

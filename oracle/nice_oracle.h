@@ -54,6 +54,16 @@ void nice_oracle_gen_syn_v1(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uin
 void nice_oracle_gen_gradient(uint8_t *px, uint32_t W, uint32_t H, uint32_t C);
 uint64_t nice_oracle_calc_pos_from(uint64_t width, uint64_t height, uint64_t index);
 void nice_oracle_gen_deep_codes(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K);
+/* encode, plus px_bit[i] = stream bit of coded pixel i's first symbol (UINT64_MAX: run member),
+ * px_bit[W*H] = the data end bit */
+int nice_oracle_encode_bitpos(const uint8_t *in, size_t in_len, uint32_t width, uint32_t height,
+                              uint8_t channels, uint8_t **out, size_t *out_len, uint64_t *px_bit);
+/* as gen_deep_codes_at; rows [flat_y0, flat_y1) one flat colour (a run) */
+void nice_oracle_gen_deep_codes_flat(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
+                                     const uint64_t *force, size_t n_force, uint32_t flat_y0, uint32_t flat_y1);
+/* RGB-mode frame with geometric residuals per channel; rows noise[] (ascending) uniform noise */
+void nice_oracle_gen_rgb_field(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed,
+                               const uint32_t *noise, size_t n_noise);
 /* as gen_deep_codes; pixels force[0..n_force) (ascending) take the rarest symbols */
 void nice_oracle_gen_deep_codes_at(uint8_t *px, uint32_t W, uint32_t H, uint32_t C, uint32_t seed, uint32_t K,
                                    const uint64_t *force, size_t n_force);

@@ -104,6 +104,15 @@ def lib():
         L.nice_oracle_gen_deep_codes_at.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                     ctypes.c_uint32, ctypes.c_uint32,
                                                     ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
+        L.nice_oracle_encode_bitpos.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint8, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                                ctypes.POINTER(ctypes.c_uint64)]
+        L.nice_oracle_gen_deep_codes_flat.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                      ctypes.c_uint32, ctypes.c_uint32,
+                                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                                                      ctypes.c_uint32, ctypes.c_uint32]
+        L.nice_oracle_gen_rgb_field.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -130,6 +139,26 @@ def encode(px: np.ndarray, width: int, height: int, channels: int, channels_out=
     finally:
         L.nice_oracle_free(out)
     return (data, st) if with_stats else data
+
+
+def encode_bitpos(px: np.ndarray, width: int, height: int, channels: int):
+    """encode() plus, per pixel, the stream bit where its first symbol starts
+    (2**64-1 for run members), then the data end bit: (stream, uint64 array
+    of W*H + 1)."""
+    L = lib()
+    px = np.ascontiguousarray(px, dtype=np.uint8).reshape(-1)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    bits = np.zeros(width * height + 1, dtype=np.uint64)
+    rc = L.nice_oracle_encode_bitpos(_u8p(px), px.size, width, height, channels, ctypes.byref(out),
+                                     ctypes.byref(n), bits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed rc={rc}")
+    try:
+        data = bytes(ctypes.string_at(out, n.value))
+    finally:
+        L.nice_oracle_free(out)
+    return data, bits
 
 
 def decode(stream: bytes, mode: int = DEC_REFERENCE):
@@ -196,6 +225,28 @@ def gen_deep_codes_at(width: int, height: int, channels: int, seed: int, k: int,
     f = np.ascontiguousarray(sorted(force), dtype=np.uint64)
     lib().nice_oracle_gen_deep_codes_at(_u8p(px), width, height, channels, seed, k,
                                         f.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), f.size)
+    return px
+
+
+def gen_deep_codes_flat(width: int, height: int, channels: int, seed: int, k: int, force,
+                        flat_rows) -> np.ndarray:
+    """gen_deep_codes_at with rows [flat_rows[0], flat_rows[1]) one flat colour
+    (a single run, generated without disturbing the symbol counts)."""
+    px = np.zeros(width * height * channels, dtype=np.uint8)
+    f = np.ascontiguousarray(sorted(force), dtype=np.uint64)
+    lib().nice_oracle_gen_deep_codes_flat(_u8p(px), width, height, channels, seed, k,
+                                          f.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), f.size,
+                                          flat_rows[0], flat_rows[1])
+    return px
+
+
+def gen_rgb_field(width: int, height: int, channels: int, seed: int, noise_rows) -> np.ndarray:
+    """RGB-mode frame (geometric residuals per channel) with uniform-noise rows
+    ``noise_rows``: the noise pixels cost over 32 bits each."""
+    px = np.zeros(width * height * channels, dtype=np.uint8)
+    r = np.ascontiguousarray(sorted(noise_rows), dtype=np.uint32)
+    lib().nice_oracle_gen_rgb_field(_u8p(px), width, height, channels, seed,
+                                    r.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), r.size)
     return px
 
 

@@ -1,0 +1,73 @@
+"""enc_pack's over-cap path (hfe.rs:110-113, bitwriter.rs:55-73).
+
+A packer group (4 tiles, 4096 pixels) collects its codes in an LDS buffer of
+32 bits per pixel.  A group that goes over it -- only possible after its first
+tiles have already been OR-ed into the buffer -- is counted and OR-ed into the
+output directly instead, and the next group on the block must clear the whole
+buffer.  NICE_ENC_PACK_CAP=b lowers the buffer to b bits per pixel so ordinary
+frames reach that path (mid-group, after tiles were written); a frame with one
+row of noise in a smooth image reaches it at the real cap.  Every stream must
+equal the oracle's byte for byte.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cap", [4, 8, 12])
+def test_pack_cap_single_frames(nice, O, cap, monkeypatch):
+    monkeypatch.setenv("NICE_ENC_PACK_CAP", str(cap))
+    for w, h, c, seed in [(1920, 1080, 4, 3), (4096, 64, 4, 5), (1000, 333, 3, 2)]:
+        px = O.gen_syn_v1(w, h, c, seed)
+        want = O.encode(px, w, h, c)
+        got = nice.encode_bytes(px, w, h, c)
+        assert got == want, (w, h, c, cap)
+
+
+def test_pack_cap_batch(nice, O, monkeypatch):
+    """A batch: blocks move between frames and reuse their LDS buffer across
+    over-cap and ordinary groups."""
+    import torch
+    monkeypatch.setenv("NICE_ENC_PACK_CAP", "11")   # SYN-v1 averages ~10.7 bits/px: both kinds of group
+    w, h, c, n = 1280, 720, 4, 6
+    frames = np.stack([O.gen_syn_v1(w, h, c, s) for s in range(1, n + 1)])
+    px = torch.from_numpy(frames).cuda()
+    bound = (nice.encode_bound(w, h) + 255) // 256 * 256
+    out = torch.zeros((n, bound), dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(n, dtype=torch.int64, device="cuda")
+    nice.encode_batch(px, w, h, c, out, lens)
+    torch.cuda.synchronize()
+    L = lens.cpu().numpy()
+    host = out.cpu().numpy()
+    for i in range(n):
+        want = O.encode(frames[i], w, h, c)
+        assert bytes(host[i, :L[i]]) == want, i
+
+
+def test_pack_cap_bands(nice, O, monkeypatch):
+    import torch
+    from conftest import band_encode
+    monkeypatch.setenv("NICE_ENC_PACK_CAP", "8")
+    w, h, c = 2048, 512, 4
+    px = O.gen_syn_v1(w, h, c, 4)
+    want = O.encode(px, w, h, c)
+    got = band_encode(nice, torch.from_numpy(px).cuda(), w, h, c, 3).cpu().numpy().tobytes()
+    assert got == want
+
+
+def test_pack_noise_row_real_cap(nice, O):
+    """Rows of uniform noise in a 4096-wide frame of RGB-mode pixels with
+    geometric residuals (oracle gen_rgb_field): each noise row is one packer
+    group whose residuals take the rare 15-17 bit codes of stream 0, about 50
+    bits per pixel, so the group goes over the real cap after its first tiles;
+    the groups after it reuse the buffer."""
+    w, h, c = 4096, 1024, 4
+    px = O.gen_rgb_field(w, h, c, 1, [300, 301, 400])
+    want, st = O.encode(px, w, h, c, with_stats=True)
+    assert st.max_emitted_aob <= 25   # not a long-code frame: the one-pass packer runs
+    aob = np.array(st.aob[0:256])
+    rare = aob[np.array(st.hist[0:256]) > 0].max()
+    assert 3 * rare > 40, rare        # a noise pixel: prefix + three rare residuals
+    got = nice.encode_bytes(px, w, h, c)
+    assert got == want

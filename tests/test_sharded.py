@@ -210,3 +210,143 @@ def test_sharded_error_every_rank_raises(tmp_path, fail):
     res = _run_mock(tmp_path, list(fail), port)
     assert all("error" in d for d in res), res
     assert all(("nice_band_" + fail[1]) in d["error"] for d in res), res
+
+
+# ---- eight-rank rehearsal with real band bit counts (CPU, gloo) -------------
+ORACLE_WORKER = textwrap.dedent("""
+    import importlib, json, sys
+    sys.path.insert(0, {root!r})
+    import numpy as np, torch, torch.distributed as dist
+    from oracle import oracle as O
+    S = importlib.import_module({pkg!r} + ".sharded")
+
+    W, H, C = 2048, 2048, 4
+    N = W * H
+    MAX = np.uint64(2**64 - 1)
+
+    def image(R):
+        # Fibonacci-skewed small diffs (codes up to 29 bits), the rarest
+        # symbols forced onto the first pixels of bands 1 and 2; rows
+        # 700..1039 one flat colour: a run from band 2 across all of band 3
+        # (no coded pixel: 0 bits) into band 4
+        starts = [S.band_tiles(W, H, r, R)[0] * 1024 for r in range(R)]
+        return O.gen_deep_codes_flat(W, H, C, 1, 29, [starts[1], starts[2]], (700, 1040))
+
+    class OracleBands:
+        # the band steps restated from the oracle's whole-image stream: a band's
+        # bits are [bit of its first coded pixel, bit of the next band's), its
+        # words that slice at its stream word positions (nice_band_words)
+        def __init__(self, px, R):
+            self.px, self.R = px, R
+            self.stream, self.bit = O.encode_bitpos(px, W, H, C)
+            _, st = O.encode(px, W, H, C, with_stats=True)
+            self.hist = np.array(st.hist, dtype=np.int64)
+            self.coded = np.nonzero(self.bit[:N] != MAX)[0]
+        def _first_from(self, p):
+            k = np.searchsorted(self.coded, p)
+            return int(self.coded[k]) if k < len(self.coded) else None
+        def classify(self, px, px0, w, h, c, co, lo, hi):
+            self.lo, self.hi = lo * 1024, min(hi * 1024, N)
+            k0, k1 = np.searchsorted(self.coded, [self.lo, self.hi])
+            f = int(self.coded[k0]) if k1 > k0 else S.NONE
+            l = int(self.coded[k1 - 1]) if k1 > k0 else S.NONE
+            return torch.tensor([f, l], dtype=torch.int64)
+        def runs(self, band_next):
+            self.band_next = int(band_next)
+            r = dist.get_rank()
+            part = self.hist // self.R + (self.hist % self.R if r == 0 else 0)
+            return torch.from_numpy(part.astype(np.int32))
+        def tables(self, hist):
+            self.hist_ok = bool(np.array_equal(hist.numpy().astype(np.int64), self.hist))
+            f = self._first_from(self.lo)
+            start = int(self.bit[f]) if f is not None and f < self.hi else None
+            nxt = self._first_from(self.hi)
+            end = int(self.bit[nxt]) if nxt is not None else int(self.bit[N])
+            bits = end - start if start is not None else 0
+            return torch.tensor([bits, int(self.bit[0])], dtype=torch.int64)
+        def words(self, bit0, bits):
+            return ((bit0 + bits + 31) >> 5) - (bit0 >> 5) + 2 if bits else 0
+        def pack(self, bit0, bits):
+            n = self.words(bit0, bits)
+            if not n:
+                return torch.zeros(0, dtype=torch.int32)
+            allb = np.unpackbits(np.frombuffer(self.stream, np.uint8))
+            w0 = (bit0 >> 5) * 32
+            buf = np.zeros((n - 2) * 32, np.uint8)
+            buf[bit0 - w0: bit0 - w0 + bits] = allb[bit0: bit0 + bits]
+            wd = np.packbits(buf).view(">u4").astype(np.int64)
+            return torch.from_numpy(np.concatenate([wd, [0, 0]]).astype(np.uint32).view(np.int32))
+        def assemble(self, cat, bit0s, bitss, w, h):
+            seed, end = bit0s[0], bit0s[0] + sum(bitss)
+            out = np.zeros(((end + 31) >> 5) * 32 + 64, np.uint8)
+            out[:seed] = np.unpackbits(np.frombuffer(self.stream, np.uint8))[:seed]   # the root's header
+            words = cat.numpy().view(np.uint32)
+            off = 0
+            for b0, b in zip(bit0s, bitss):
+                n = self.words(b0, b)
+                if n:
+                    seg = np.unpackbits(words[off: off + n - 2].astype(">u4").view(np.uint8))
+                    out[(b0 >> 5) * 32: (b0 >> 5) * 32 + seg.size] |= seg
+                off += n
+            by = np.packbits(out[:end + (-end) % 8]).tobytes()
+            B = end >> 3
+            P = by[B] if end & 7 else 0
+            return by[:B] + bytes([P, P, 0, 0, 0])
+
+    dist.init_process_group("gloo")
+    r, R = dist.get_rank(), dist.get_world_size()
+    px = image(R)
+    be = OracleBands(px, R)
+    out = S.encode_sharded(be, dist, torch.zeros(4), 0, W, H, C, device="cpu")
+    res = {{"rank": r, "band_next": be.band_next, "hist_ok": be.hist_ok, "lo": be.lo}}
+    if r == 0:
+        res["equal"] = out == be.stream
+        res["len"] = len(be.stream)
+    got = [None] * R
+    dist.all_gather_object(got, res)
+    if r == 0:
+        # per-band bits and first-pixel cost, from the same oracle data
+        info = []
+        for q in range(R):
+            lo, hi = S.band_tiles(W, H, q, R)
+            lo, hi = lo * 1024, min(hi * 1024, N)
+            f = be._first_from(lo)
+            nb = None if f is None or f >= hi else be._first_from(f + 1)
+            cost = int(be.bit[nb] - be.bit[f]) if nb is not None else None
+            info.append({{"first": f if f is not None and f < hi else None, "first_cost": cost}})
+        print(json.dumps({{"ranks": got, "bands": info}}))
+    dist.destroy_process_group()
+""")
+
+
+def test_sharded_exchange_gloo_8_ranks(tmp_path, O):
+    """encode_sharded's exchange at world size 8 (the config-4 split) over
+    gloo, with band steps restated from the oracle's whole-image stream (real
+    bit counts, so bands start at arbitrary bit offsets): a 2048^2 frame with
+    ~30-bit codes, the rarest forced onto band starts, and a flat region whose
+    run starts in band 2, covers all of band 3 (0 bits) and ends in band 4.
+    The root's assembled stream must equal the oracle's whole-image encode.
+    (The same split runs on the GPU's band API in test_configs /
+    test_long_codes; this covers the rank exchange at the driver's 8 ranks.)"""
+    import json
+    script = tmp_path / "w8.py"
+    script.write_text(ORACLE_WORKER.format(root=ROOT, pkg=PKG_NAME))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                          "--master-addr", "127.0.0.1", "--master-port", "29671", str(script)],
+                         capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    ranks = sorted(res["ranks"], key=lambda d: d["rank"])
+    bands = res["bands"]
+    print(bands)
+    assert ranks[0]["equal"], "assembled stream differs from the oracle's"
+    assert all(d["hist_ok"] for d in ranks)
+    # band 3 lies inside the run: no coded pixel, so band 2's runs end in band 4
+    assert bands[3]["first"] is None
+    assert ranks[2]["band_next"] == ranks[3]["band_next"] == bands[4]["first"]
+    assert bands[4]["first"] >= 1040 * 2048
+    # bands 1 and 2 start with the rarest symbols: a pixel of >= 28 bits, a
+    # 1-2 bit small-diff prefix and a small-diff code of over 25 bits (the
+    # reference writer's wrapped write, bitwriter.rs:55-73)
+    assert all(bands[q]["first"] == ranks[q]["lo"] and bands[q]["first_cost"] >= 28 for q in (1, 2))

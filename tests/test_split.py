@@ -109,3 +109,78 @@ def test_row_segment_sizes(nice, O, seg, monkeypatch):
     for name, px, w, h, c in _cases(O) + [("syn64x9x3", O.gen_syn_v1(64, 9, 3, 2), 64, 9, 3),
                                           ("syn2047x12x4", O.gen_syn_v1(2047, 12, 4, 3), 2047, 12, 4)]:
         assert _check(nice, O, px, w, h, c), (name, seg)
+
+
+def _split_stats(nice, ctx):
+    import ctypes
+    L = nice.lib()
+    L.nice_test_split_redos.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
+    nf, nr = ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.nice_test_split_redos(ctx.ptr, ctypes.byref(nf), ctypes.byref(nr)) == 0
+    return nf.value, nr.value
+
+
+def _decode_dev(nice, O, px, w, h, c, ctx, stream=None):
+    import torch
+    s = O.encode(px, w, h, c)
+    sb = torch.zeros((1, (len(s) + 255) // 256 * 256), dtype=torch.uint8)
+    sb[0, :len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
+    sb = sb.cuda()
+    lens = torch.tensor([len(s)], dtype=torch.int64, device="cuda")
+    dec = torch.zeros((1, w * h * 4), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    nice.decode_batch(sb, lens, w, h, 4, dec, status, flags=nice.DEC_ALPHA_FILL_FF | nice.DEC_TOLERANT_HEADER,
+                      stream=stream, ctx=ctx)
+    return dec, status
+
+
+def test_split_wider_than_16384(nice, O):
+    """W > 16384 (one workgroup cannot hold a row's segments) decodes through
+    the strip split too (was: the 64-lane dec_reconstruct)."""
+    import torch
+    w, h, c = 20000, 48, 4
+    px = O.gen_syn_v1(w, h, c, 21)
+    ctx = nice.Context(0)
+    dec, status = _decode_dev(nice, O, px, w, h, c, ctx)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0
+    assert np.array_equal(dec[0].view(-1, 4)[:, :3].cpu().numpy(), px.reshape(-1, 4)[:, :3])
+    nf, nr = _split_stats(nice, ctx)
+    assert nf == 1 and nr == 0
+
+
+def test_split_not_coresident_falls_back(nice, O):
+    """A 16384-wide decode while another stream's kernel holds every CU but
+    one for 1.5 s: the strips cannot all be resident, the first one's wait
+    times out, and the frame is reconstructed by the fallback launch -- exact
+    pixels, status 0, no NICE_E_HIP."""
+    import ctypes
+    import torch
+    w, h, c = 16384, 64, 4
+    px = O.gen_syn_v1(w, h, c, 22)
+    ctx = nice.Context(0)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    L = nice.lib()
+    L.nice_test_occupy.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 5
+    busy = torch.cuda.Stream()
+    work = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    # one block per CU (96 KB of LDS each: no 82 KB strip block fits beside it);
+    # one CU frees after 20 ms, the rest after 1.5 s
+    assert L.nice_test_occupy(ctypes.c_void_p(busy.cuda_stream), cus, 1, 20000, 1500000, 96 * 1024) == 0
+    t0 = time.time()
+    dec, status = _decode_dev(nice, O, px, w, h, c, ctx, stream=work)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    assert int(status[0]) == 0
+    assert np.array_equal(dec[0].view(-1, 4)[:, :3].cpu().numpy(), px.reshape(-1, 4)[:, :3])
+    nf, nr = _split_stats(nice, ctx)
+    assert nf == 1
+    print(f"decode beside the occupying kernel: {dt:.2f} s, frames redone: {nr}")
+    # the same context decodes normally afterwards (split, no fallback)
+    dec, status = _decode_dev(nice, O, px, w, h, c, ctx)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0
+    assert _split_stats(nice, ctx) == (1, 0)
