@@ -277,6 +277,51 @@ def rgb_leg(torch, nice, device, W, H, F, check, reps=3):
             "stream_check": None if exact is None else "oracle, last frame: byte-exact"}
 
 
+def batch_leg(torch, nice, device, W, H, F, seed0, check, reps=3, what="config3"):
+    """A batch of F W x H RGBA SYN-v1 frames resident in HBM (BASELINE config 3:
+    64 x 1920x1080, per-image parallelism on one GPU; also 8K UHD frames):
+    encode-only, decode-only and encode-then-decode rates; the last frame's
+    stream byte-compared with the oracle and the round trip checked (outside
+    the timed regions)."""
+    N = W * H
+    px = syn_frames(torch, F, W, H, seed0, device)
+    stride = (nice.encode_bound(W, H) + 255) // 256 * 256
+    streams = torch.empty((F, stride), dtype=torch.uint8, device=device)
+    lens = torch.zeros(F, dtype=torch.int64, device=device)
+    dec = torch.empty((F, N * 4), dtype=torch.uint8, device=device)
+    status = torch.zeros(F, dtype=torch.int32, device=device)
+    ctx = nice.Context(device.index or 0)
+    enc = lambda: nice.encode_batch(px, W, H, 4, streams, lens, ctx=ctx)
+    dcd = lambda: nice.decode_batch(streams, lens, W, H, 4, dec, status, ctx=ctx)
+    enc()
+    dcd()
+    torch.cuda.synchronize()
+    assert int(status.abs().sum()) == 0, f"{what}: decode status"
+    assert torch.equal(dec.view(F, N, 4)[:, :, :3], px.view(F, N, 4)[:, :, :3]), f"{what}: round trip"
+    exact = None
+    if check:
+        from oracle import oracle as O
+        want = O.encode(px[F - 1].cpu().numpy(), W, H, 4)
+        exact = streams[F - 1, :int(lens[F - 1])].cpu().numpy().tobytes() == want
+        assert exact, f"{what}: stream differs from the oracle"
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps
+    t_e, t_d = timed(enc), timed(dcd)
+    t_ed = timed(lambda: (enc(), dcd()))
+    return {"workload": f"{F} x {W}x{H} RGBA SYN-v1 frames (seeds {seed0}..{seed0 + F - 1}), inputs resident in HBM",
+            "encode_mpix_s": round(F * N / t_e / 1e6, 1), "decode_mpix_s": round(F * N / t_d / 1e6, 1),
+            "encode_decode_mpix_s": round(F * N / t_ed / 1e6, 1),
+            "encode_ms": round(t_e * 1e3, 3), "decode_ms": round(t_d * 1e3, 3),
+            "bits_per_pixel": round(int(lens.sum()) * 8 / (F * N), 3),
+            "stream_check": None if exact is None else "oracle, last frame: byte-exact, round trip exact"}
+
+
 def gpu_numa_cpus(torch, device):
     """(NUMA node, its CPUs) of the GPU's PCIe root from sysfs, or (None, None)."""
     try:
@@ -425,6 +470,10 @@ def main():
                          "in 8 bands on one GPU (N=1) (0: skip)")
     ap.add_argument("--rgb-frames", type=int, default=128,
                     help="4K RGB leg: frames per GPU encoded and decoded (0: skip)")
+    ap.add_argument("--config3-frames", type=int, default=64,
+                    help="BASELINE config 3 leg: 1920x1080 RGBA frames per GPU (0: skip)")
+    ap.add_argument("--uhd8k-frames", type=int, default=16,
+                    help="8K UHD leg: 7680x4320 RGBA frames per GPU (0: skip)")
     ap.add_argument("--check-frames", type=int, default=4,
                     help="frames of the timed batch byte-compared with the oracle (rank 0)")
     ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)
@@ -543,6 +592,23 @@ def main():
             rgb = {"error": repr(exc)[:300]}
         torch.cuda.empty_cache()
 
+    config3 = None
+    if args.config3_frames:
+        try:
+            config3 = batch_leg(torch, nice, device, 1920, 1080, args.config3_frames, 1 + rank * args.config3_frames,
+                                rank == 0 and args.check_frames > 0)
+        except Exception as exc:   # report, never lose the main measurement
+            config3 = {"error": repr(exc)[:300]}
+        torch.cuda.empty_cache()
+    uhd8k = None
+    if args.uhd8k_frames:
+        try:
+            uhd8k = batch_leg(torch, nice, device, 7680, 4320, args.uhd8k_frames, 7001 + rank * args.uhd8k_frames,
+                              rank == 0 and args.check_frames > 0, what="8k")
+        except Exception as exc:   # report, never lose the main measurement
+            uhd8k = {"error": repr(exc)[:300]}
+        torch.cuda.empty_cache()
+
     stream_leg = None
     if args.streamed_frames:
         try:
@@ -616,6 +682,8 @@ def main():
         "stream_check": check,
         "subblock_positions": subblock,
         "rgb_4k": rgb,
+        "config3_batch_1080p": config3,   # BASELINE config 3
+        "uhd8k_7680x4320": uhd8k,
         "stream_bytes_per_frame": stream_bytes // F,
         "bits_per_pixel": round(stream_bytes * 8 / (F * N), 3),
         "phase_ms_timed_region": phase,

@@ -53,7 +53,7 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Encoder scratch layout. The zero-per-launch block comes first (memset once).
 struct EncLayout {
   size_t zero_bytes, total;
-  size_t o_hist, o_flags, o_ctr, o_status;
+  size_t o_hist, o_flags, o_ctr, o_status, o_overn, o_overl;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
       o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc, o_bhist;
 };
@@ -66,7 +66,9 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   L.o_flags = take((size_t)n_frames * 4 + 4);   // + one word: any frame FLAG_LONG
   L.o_ctr = take((size_t)n_frames * 4);
   L.o_status = take((size_t)n_frames * T * 8);
+  L.o_overn = take(4);
   L.zero_bytes = align_up(o, 16);
+  L.o_overl = take((size_t)n_frames * ((T + PACK_SUB - 1) / PACK_SUB) * 8);
   L.o_first = take((size_t)n_frames * T * 4);
   L.o_last = take((size_t)n_frames * T * 4);
   L.o_next = take((size_t)n_frames * T * 4);
@@ -162,6 +164,7 @@ struct nice_ctx {
   // the last split decode's per-frame abort flags (test hook nice_test_split_redos)
   const uint32_t* split_abort = nullptr;
   uint32_t split_frames = 0;
+  int last_classify = -1;   // ClsKind of the last encode / band classify (test hook nice_test_last_classify)
 };
 
 extern "C" {
@@ -277,6 +280,8 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.px_lo = 0;
   a.px_hi = (int64_t)N;
   a.band = 0;
+  a.over_count = (uint32_t*)(base + L.o_overn);
+  a.over_list = (uint2*)(base + L.o_overl);
   a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * 32;
   if (const char* ev = getenv("NICE_ENC_PACK_CAP")) {   // tests: bits per pixel of the LDS buffer
     const int b = atoi(ev);
@@ -296,6 +301,58 @@ static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, u
   if (r > rows_total) r = rows_total ? rows_total : 1;
   *blocks = (uint32_t)(n_frames * strips * ((rows_total + r - 1) / r));
   return (uint32_t)r;
+}
+
+// The classify kernel for a frame shape (every kernel writes the same
+// records, histogram and tile edges): the LDS ring (each pixel loaded once)
+// wherever the rows fit it, the strip kernel for wider RGBA rows of whole
+// tiles, the round-1 window kernel otherwise.  `aligned`: the pixel base
+// (frames: and stride) is 4-byte aligned, as the ring and strip loads need.
+enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP };
+static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
+  if (w < 3) return CLS_K_TINY;
+  if (!aligned || getenv("NICE_ENC_NO_RING")) return CLS_K_WINDOW;
+  if (w <= CLS_RING_MAX_W) return CLS_K_RING;
+  if (channels == 4 && w % ENC_TILE == 0) return CLS_K_STRIP;
+  if (w <= CLS_RING2_MAX_W) return CLS_K_RING2;
+  return CLS_K_WINDOW;
+}
+// Launches it over `work` tiles (frames x band tiles); rows_total: the rows the
+// strip kernel walks per frame.
+static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work, uint32_t rows_total,
+                            hipStream_t st) {
+  const bool ringk = k == CLS_K_RING || k == CLS_K_RING2;
+  // contiguous tile chunks per block: keeps rows-above reuse in L2 and flushes
+  // each block's LDS histogram once per frame; ring kernels: >= 16 tiles per
+  // block (the 3-row prefill amortised), 2 blocks per CU (ring2: 1)
+  uint64_t blocks = k == CLS_K_RING ? 2ull * ctx->cus : k == CLS_K_RING2 ? (uint64_t)ctx->cus : 2048;
+  uint64_t per = (work + blocks - 1) / blocks;
+  if (per < (ringk ? 16u : 1u)) per = ringk ? 16 : 1;
+  if (ringk && per > 16384) per = 16384;   // its 16-bit per-thread prefix counters
+  blocks = (work + per - 1) / per;
+  a.tiles_per_block = (uint32_t)per;
+  const bool rgb = a.C == 3;
+  switch (k) {
+    case CLS_K_STRIP: {
+      uint32_t sblocks;
+      a.tiles_per_block = strip_rows(ctx, a.n_frames, a.W, rows_total, &sblocks);
+      hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      break;
+    }
+    case CLS_K_RING:
+      if (rgb) hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      break;
+    case CLS_K_RING2:
+      if (rgb) hipLaunchKernelGGL(enc_classify_ring2_3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(enc_classify_ring2, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      break;
+    case CLS_K_TINY:
+      hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+      break;
+    default:
+      hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  }
 }
 
 extern "C" {
@@ -318,8 +375,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   hipStream_t st = (hipStream_t)stream;
   const uint32_t T = tiles_for(w, h);
   const bool aligned = ((uintptr_t)d_px & 3) == 0 && (frame_stride & 3) == 0;
-  const bool ring = aligned && w >= 3 && w <= CLS_RING_MAX_W && !getenv("NICE_ENC_NO_RING");
-  const bool strip = aligned && channels == 4 && w > CLS_RING_MAX_W && w % ENC_TILE == 0 && !getenv("NICE_ENC_NO_RING");
+  const ClsKind ck = pick_classify(w, channels, aligned);
   if ((uint64_t)n_frames * T >= (1ull << 32)) return NICE_E_ARG;   // enc_pack's 32-bit work counter
   EncLayout L = enc_layout(n_frames, T, N);
   int rc = ctx->enc.grow(L.total);
@@ -334,28 +390,10 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
   const uint64_t total_tiles = (uint64_t)n_frames * T;
   if (T > 0) {
-    // contiguous tile chunks per block: keeps rows-above reuse in L2 and
-    // flushes each block's LDS histogram once per frame
-    // RGBA frames: ring-staged kernel (each pixel loaded once; >= 16 tiles per
-    // block so the 3-row prefill is amortised, 2 blocks per CU)
-    uint64_t blocks = ring ? 512 : 2048;
-    uint64_t per = (total_tiles + blocks - 1) / blocks;
-    if (per < (ring ? 16u : 1u)) per = ring ? 16 : 1;
-    if (ring && per > 16384) per = 16384;   // its 16-bit per-thread prefix counters
-    blocks = (total_tiles + per - 1) / per;
-    a.tiles_per_block = (uint32_t)per;
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
-    if (strip) {
-      uint32_t sblocks;
-      a.tiles_per_block = strip_rows(ctx, n_frames, w, h, &sblocks);
-      hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
-    } else if (ring && channels == 4)
-      hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
-    else if (ring)
-      hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
-    else if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    launch_classify(ctx, ck, a, total_tiles, h, st);
+    ctx->last_classify = (int)ck;
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
     if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, n_frames), dim3(256), 0, st, a, 0);
@@ -387,6 +425,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     const uint64_t pblocks = std::min<uint64_t>(total_tiles, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU);
     ctx->timer.begin(NICE_PH_ENC_PACK, st);
     hipLaunchKernelGGL(enc_pack, dim3((uint32_t)pblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(enc_pack_over, dim3(PACK_OVER_BLOCKS), dim3(256), 0, st, a);
     hipLaunchKernelGGL(enc_edges, dim3(std::min<uint32_t>((T + 255) / 256, 64u), std::min<uint32_t>(n_frames, 4096u)),
                        dim3(256), 0, st, a);
     ctx->timer.end(st);
@@ -864,20 +903,14 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   a.pack_mode = 0;
   a.long_only = 1;
   NICE_HIP(hipMemsetAsync(base, 0, L.zero_bytes, st));
-  const uint64_t work = tile_hi - tile_lo;
-  uint64_t blocks = 2048, per = (work + blocks - 1) / blocks;
-  if (per < 1) per = 1;
-  blocks = (work + per - 1) / per;
-  a.tiles_per_block = (uint32_t)per;
-  if (channels == 4 && w > CLS_RING_MAX_W && w % ENC_TILE == 0 && ((uintptr_t)d_px & 3) == 0 &&
-      !getenv("NICE_ENC_NO_RING")) {
-    // the band's rows in strips (tiles outside the band are staged, not classified)
-    const uint32_t tpr = w / ENC_TILE, rows_band = (tile_hi + tpr - 1) / tpr - tile_lo / tpr;
-    uint32_t sblocks;
-    a.tiles_per_block = strip_rows(ctx, 1, w, rows_band, &sblocks);
-    hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
-  } else if (w < 3) hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+  // the ring / strip kernels read the band's pixels through the virtual base
+  // as 32-bit words: it must be 4-byte aligned
+  const ClsKind ck = pick_classify(w, channels, ((uintptr_t)a.px & 3) == 0);
+  // strip kernel: the band's rows (tiles outside the band are staged, not classified)
+  const uint32_t tpr = std::max<uint32_t>(w / ENC_TILE, 1u);
+  const uint32_t rows_band = (tile_hi + tpr - 1) / tpr - tile_lo / tpr;
+  launch_classify(ctx, ck, a, tile_hi - tile_lo, rows_band, st);
+  ctx->last_classify = (int)ck;
   hipLaunchKernelGGL(enc_band_edges, dim3(1), dim3(256), 0, st, a, d_edges);
   NICE_HIP(hipGetLastError());
   ctx->bs = BandState{};
@@ -997,6 +1030,7 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;
   NICE_HIP(hipMemsetAsync(a.status, 0, (size_t)ng * 8, st));
   NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
+  NICE_HIP(hipMemsetAsync(a.over_count, 0, 4, st));
   if (ctx->bs.d_info)   // the bit count the caller read back must be the device's
     hipLaunchKernelGGL(enc_band_check, dim3(1), dim3(64), 0, st, a, ctx->bs.d_info, (unsigned long long)band_bits);
   // FLAG_LONG (the launches return at once otherwise): tile bits, their scan from
@@ -1010,6 +1044,7 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   // every other band: one pass, group offsets by look-back from band_bit0
   hipLaunchKernelGGL(enc_pack, dim3((uint32_t)std::min<uint64_t>(nt, (uint64_t)ctx->cus * PACK_BLOCKS_PER_CU)),
                      dim3(256), 0, st, a);
+  hipLaunchKernelGGL(enc_pack_over, dim3(PACK_OVER_BLOCKS), dim3(256), 0, st, a);
   hipLaunchKernelGGL(enc_edges, dim3(std::min<uint32_t>((ng + 255) / 256, 64u), 1), dim3(256), 0, st, a);
   NICE_HIP(hipGetLastError());
   return NICE_OK;
@@ -1143,6 +1178,10 @@ int nice_test_occupy(void* stream, uint32_t blocks, uint32_t short_blocks, uint3
   NICE_HIP(hipGetLastError());
   return NICE_OK;
 }
+// The classify kernel the context's last encode (or band classify) used:
+// 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip.
+int nice_test_last_classify(nice_ctx* ctx) { return ctx ? ctx->last_classify : -1; }
+
 // Frames of the context's last split decode that went to the fallback launch
 // (synchronises the device).
 int nice_test_split_redos(nice_ctx* ctx, uint32_t* split_frames, uint32_t* redos) {

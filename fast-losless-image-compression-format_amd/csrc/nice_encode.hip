@@ -521,12 +521,12 @@ template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
                                                const uint32_t* b3, const uint32_t* rbase, uint32_t tid, uint32_t W,
                                                uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd);
-template <bool HEAD>
+template <bool HEAD, int RING = CLS_RING>
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
                                                   uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
-  return classify_y<HEAD>(ring + ((s - 3u) & (CLS_RING - 1)) + tid, ring + ((s - W - 3u) & (CLS_RING - 1)) + tid,
-                          ring + ((s - 2u * W) & (CLS_RING - 1)) + tid,
-                          ring + ((s - 3u * W - 3u) & (CLS_RING - 1)) + tid, ring, tid, W, i, ltab, cbr, csd);
+  return classify_y<HEAD>(ring + ((s - 3u) & (RING - 1)) + tid, ring + ((s - W - 3u) & (RING - 1)) + tid,
+                          ring + ((s - 2u * W) & (RING - 1)) + tid,
+                          ring + ((s - 3u * W - 3u) & (RING - 1)) + tid, ring, tid, W, i, ltab, cbr, csd);
 }
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
@@ -637,16 +637,16 @@ __device__ __forceinline__ uint32_t px_word(const uint8_t* fr, int64_t j) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
 }
 
-template <int C>
+template <int C, int RING>
 __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
-  __shared__ uint32_t ring[CLS_RING + CLS_GUARD];
+  __shared__ uint32_t ring[RING + CLS_GUARD];
   __shared__ uint32_t stage[C == 3 ? RGB_TILE_DW + 4 : 1];
   __shared__ uint32_t hs[C0_N + 2 * SX_N];     // slot histogram (nice_rec.hpp)
   __shared__ uint32_t run_hist[8];             // run digits (prefixes 5..12)
   __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t ltab[2][CLS_PPT][16];   // [tile parity][q][luma reference]: ring index for thread 0
-  const uint32_t T = a.tiles_per_frame;
-  const uint64_t total_work = (uint64_t)a.n_frames * T;
+  // work items: frame f, tile tt in [tile_lo, tile_hi) (frames: all tiles; bands: the band's)
+  const uint64_t total_work = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
   const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
   const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
   if (w_begin >= w_end) return;
@@ -676,15 +676,16 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
     if (tid < 8) run_hist[tid] = 0;
   };
   // prefill: the 3 rows + 3 pixels before the first tile
-  uint32_t cur_frame = (uint32_t)(w_begin / T);
+  TileIter it(a, w_begin), nx(a, w_begin);
+  uint32_t cur_frame = it.f;
   {
-    const int64_t start = (int64_t)(w_begin % T) * ENC_TILE;
+    const int64_t start = (int64_t)it.tt() * ENC_TILE;
     const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
     const uint8_t* fr = a.px + (uint64_t)cur_frame * a.frame_stride;
     for (int64_t j = lo + tid; j < start; j += CLS_THREADS) {
-      const uint32_t k = (uint32_t)j & (CLS_RING - 1), y = y_from_rgba(px_word<C>(fr, j));
+      const uint32_t k = (uint32_t)j & (RING - 1), y = y_from_rgba(px_word<C>(fr, j));
       ring[k] = y;
-      if (k < CLS_GUARD) ring[CLS_RING + k] = y;
+      if (k < CLS_GUARD) ring[RING + k] = y;
     }
   }
   // the first tile's pixels
@@ -707,9 +708,17 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
                  ? rgb_dword(fr, nbytes, j0 + CLS_THREADS + tid) : 0u;
     }
   };
-  TileIter it(a, w_begin), nx(a, w_begin);
+  // two tiles in flight: tile w is staged from one register set while tiles
+  // w + 1 (the other set) and w + 2 (refilling this one) load -- one tile of
+  // classify work did not cover the HBM latency under load.  The loop body is
+  // written once and instantiated for each set, so no register copy waits on
+  // a load still in flight.
+  uint32_t pb[CLS_PPT];
   fetch(nx, pf);
-  for (uint64_t w = w_begin; w < w_end; ++w, it.step(1)) {
+  nx.step(1);
+  if (w_begin + 1 < w_end) fetch(nx, pb);
+  nx.step(1);
+  auto tile = [&](const uint64_t w, uint32_t (&pf)[CLS_PPT]) {
     const uint32_t f = it.f;
     const uint32_t tt = it.tt();
     if (f != cur_frame) {
@@ -735,17 +744,17 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
     }
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
-      const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (CLS_RING - 1), y = y_from_rgba(pxw[q]);
+      const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1), y = y_from_rgba(pxw[q]);
       ring[k] = y;
-      if (k < CLS_GUARD) ring[CLS_RING + k] = y;
+      if (k < CLS_GUARD) ring[RING + k] = y;
     }
     // this tile's luma reference table (double-buffered: the previous tile's
     // readers are past the staging barrier below before it is rewritten)
     if (tid < 16 * CLS_PPT)
       ltab[w & 1][tid >> 4][tid & 15] =
-          ((uint32_t)(start + (tid >> 4) * CLS_THREADS) - lback) & (CLS_RING - 1);
+          ((uint32_t)(start + (tid >> 4) * CLS_THREADS) - lback) & (RING - 1);
+    if (w + 2 < w_end) fetch(nx, pf);
     nx.step(1);
-    if (w + 1 < w_end) fetch(nx, pf);
     __syncthreads();
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
@@ -754,7 +763,7 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
     for (int q = 0; q < CLS_PPT; ++q) {
       const int p = q * CLS_THREADS + tid;
       const int64_t i = start + p;
-      const uint32_t* bl = ring + ((uint32_t)(start + q * CLS_THREADS - 1) & (CLS_RING - 1)) + tid;
+      const uint32_t* bl = ring + ((uint32_t)(start + q * CLS_THREADS - 1) & (RING - 1)) + tid;
       const bool coded = p < count && (i == 0 || bl[1] != bl[0]);
       const unsigned long long bal = __ballot(coded);
       wbal[q] = bal;
@@ -770,7 +779,7 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
       const uint32_t mw = tid < ENC_TILE / 32 ? mask[tid] : 0u;
       const unsigned long long nz = __ballot(mw != 0);
       if (tid == 0) {
-        const uint64_t t = (uint64_t)f * T + tt;
+        const uint64_t t = it.tile();
         uint32_t first = NONE, last = NONE;
         if (nz) {
           const int fw = __builtin_ctzll(nz), lw = 63 - __builtin_clzll(nz);
@@ -790,10 +799,10 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
       const bool coded = (coded_bits >> q) & 1u;
       uint32_t rf;
       if (fast)   // block-uniform: both variants are straight-line code
-        rf = classify_ring<false>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q],
+        rf = classify_ring<false, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q],
                                   cbr, csd);
       else
-        rf = classify_ring<true>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p),
+        rf = classify_ring<true, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p),
                                  nullptr, cbr, csd);
       rec[q] = coded ? rf : cunc;
     }
@@ -821,11 +830,24 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
         }
       }
     }
+  };
+  for (uint64_t w = w_begin; w < w_end; w += 2) {
+    tile(w, pf);
+    it.step(1);
+    if (w + 1 < w_end) {
+      tile(w + 1, pb);
+      it.step(1);
+    }
   }
   flush(cur_frame);
 }
-__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4>(a); }
-__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4, CLS_RING>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3, CLS_RING>(a); }
+// a 32K-pixel ring (128 KB, one block per CU) for rows of up to
+// CLS_RING2_MAX_W pixels: RGBA widths the strip kernel does not take (W %
+// 1024 != 0, e.g. 7680 for 8K UHD) and RGB frames
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2(EncArgs a) { enc_classify_ring_body<4, 2 * CLS_RING>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_3(EncArgs a) { enc_classify_ring_body<3, 2 * CLS_RING>(a); }
 
 // ---------------------------------------------------------------------------
 // K1s: classify, strip-staged (RGBA frames with W % 1024 == 0 too wide for the
@@ -1870,14 +1892,158 @@ __device__ __forceinline__ void quad_emit(const PackTab& tab, const TileQuad& Q,
 }
 
 // One work item of enc_pack is PACK_SUB consecutive tiles of a frame (a
-// "group"): one claim and one look-back per 4096 pixels.  The group's codes
-// go into the LDS bit buffer tile by tile; its status word, offset and edge
-// word are those of its first tile.  A group of over PACK_CAP_BITS bits (over
-// 32 bits per pixel on average) is counted first and then OR-ed into the
-// output directly.
+// "group"): one claim and one look-back per 4096 pixels.  Wave k of the block
+// packs tile k of the group: lane L owns pixels 16L .. 16L + 15 of the tile
+// (four 16-byte record loads), composes each pixel's codes into one value of
+// <= 32 bits (T0, T1, T2, the first two run digits; a pixel with longer codes
+// puts its entries one by one), and a wave prefix sum of the lanes' bit
+// counts gives each lane's bit position in its tile.  The group's tile totals
+// (one block barrier) place the tiles in the group's LDS bit buffer; each
+// lane streams its pieces MSB-first through a 64-bit register window and ORs
+// each completed word into the buffer once: about 6 LDS atomics per 16 pixels
+// (round 3's per-4-pixel puts made two per pixel, and spent 45 % of the LDS
+// cycles in bank conflicts) and two block barriers per group instead of three
+// per tile.  A group of over pack_cap_bits bits (over 32 per pixel on average)
+// is counted first and then OR-ed into the output directly, tile by tile.
+constexpr int PW_PX = ENC_TILE / 64;   // pixels per lane: 16
+
+struct LanePx {
+  uint32_t v[PW_PX];     // composed codes (exact where the pixel's length <= 32)
+  uint32_t tot4[PW_PX / 4];   // lengths (<= 128: 8 bits each, four per word)
+  const uint32_t* rp;    // the lane's records (re-read for pixels over 32 bits)
+  uint32_t cm;           // coded flags of the lane's pixels
+  uint32_t after;        // first coded pixel after the lane (absolute)
+  uint32_t s;            // the lane's first pixel (absolute)
+  uint32_t nb, tmax, xany;
+  __device__ __forceinline__ uint32_t tot(int q) const { return (tot4[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
+};
+
+// run after pixel q of the lane (0 for run members)
+__device__ __forceinline__ uint32_t lane_run(const LanePx& P, int q) {
+  const uint32_t later = P.cm >> (q + 1);
+  const uint32_t nxt = later ? P.s + (uint32_t)(q + 1) + (uint32_t)__builtin_ctz(later) : P.after;
+  return ((P.cm >> q) & 1u) ? nxt - (P.s + (uint32_t)q) - 1u : 0u;
+}
+__device__ __forceinline__ uint32_t rc_index(uint32_t run) {
+  const uint32_t m = run - 1u;
+  return run == 0 ? RC_NONE : m < 64u ? m : RC_TWO + (m & 63u);
+}
+
+// The lane's 16 pixels of tile tt of frame f: each pixel's composed code and
+// length, the lane's bit count.  Pixel indices are < 2^30 (the boundary's
+// frame cap): 32-bit arithmetic.
+__device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab, uint32_t f, uint32_t tt,
+                                           uint32_t next_tile_px, int lane, LanePx& P) {
+  const int64_t N = (int64_t)a.W * a.H;
+  const int64_t start = (int64_t)tt * ENC_TILE;
+  const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
+  const int p0 = PW_PX * lane;
+  P.rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
+  uint32_t rec[PW_PX];
+  if (p0 + PW_PX <= count) {
+#pragma unroll
+    for (int q = 0; q < PW_PX / 4; ++q) {
+      const uint4 r = reinterpret_cast<const uint4*>(P.rp)[q];
+      rec[4 * q] = r.x; rec[4 * q + 1] = r.y; rec[4 * q + 2] = r.z; rec[4 * q + 3] = r.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < PW_PX; ++q) rec[q] = (p0 + q < count) ? P.rp[q] : rec2_unc(0);
+  }
+  P.cm = 0;
+#pragma unroll
+  for (int q = 0; q < PW_PX; ++q) P.cm |= (rec2_coded(rec[q]) ? 1u : 0u) << q;
+  // the first coded pixel after the lane: in the next lane with one, else after the tile
+  const unsigned long long lanes = __ballot(P.cm != 0u);
+  const unsigned long long later = lane < 63 ? lanes >> (lane + 1) : 0ull;
+  const int nl = later ? lane + 1 + (int)__builtin_ctzll(later) : 64;
+  const uint32_t first_local = P.cm ? (uint32_t)p0 + (uint32_t)__builtin_ctz(P.cm) : 0u;
+  const uint32_t nf = (uint32_t)__shfl((int)first_local, nl & 63);
+  P.s = (uint32_t)start + (uint32_t)p0;
+  P.after = nl < 64 ? (uint32_t)start + nf : next_tile_px;
+  P.nb = 0;
+  P.tmax = 0;
+  P.xany = 0;
+#pragma unroll
+  for (int q = 0; q < PW_PX; ++q) {
+    if ((q & 3) == 0) {
+      P.tot4[q >> 2] = 0;
+      __builtin_amdgcn_sched_barrier(0);   // four pixels' lookups in flight at a time (registers)
+    }
+    const uint32_t r = rec[q];
+    const uint32_t run = lane_run(P, q);
+    const uint2 e0 = pt_entry(tab, r, 0), e1 = pt_entry(tab, r, 1), e2 = pt_entry(tab, r, 2);
+    const uint2 e3 = tab.rc[rc_index(run)];
+    P.xany |= run > 64u ? 1u << q : 0u;
+    const uint32_t t = e0.y + e1.y + e2.y + e3.y;
+    uint32_t v = e0.x;   // exact when t <= 32 (shifts stay below 32 then)
+    v = (v << (e1.y & 31u)) | e1.x;
+    v = (v << (e2.y & 31u)) | e2.x;
+    v = (v << (e3.y & 31u)) | e3.x;
+    asm volatile("" : "+v"(v) : "v"(t));   // materialise the pixel's code now (no entries kept live)
+    P.v[q] = v;
+    P.tot4[q >> 2] |= t << (8 * (q & 3));
+    P.tmax = max(P.tmax, t);
+    P.nb += t;
+  }
+  for (uint32_t m = P.xany; m; m &= m - 1u) {   // run digits past a long run's first two (runs of >= 65)
+    for (uint32_t xr = (lane_run(P, __builtin_ctz(m)) - 1u) >> 6; xr;) {
+      P.nb += tab.rc[xr & 7u].y;
+      if (xr < 8) break;
+      xr >>= 3;
+    }
+  }
+}
+
+// The lane's codes MSB-first from bit `pos` of the group's LDS buffer
+// (bitwriter.rs:55-73 placement): a 64-bit window of pending bits, each
+// completed word OR-ed in once (the first and last are shared with the
+// neighbouring lanes; the buffer is zero).
+__device__ __forceinline__ void lane_emit(const PackTab& tab, const LanePx& P, uint32_t* bits, uint32_t pos) {
+  unsigned long long acc = 0;
+  uint32_t n = pos & 31u, wi = pos >> 5;
+  auto put = [&](uint32_t val, uint32_t len) {   // len <= 32, val < 2^len
+    acc = (acc << len) | val;
+    n += len;
+    if (n >= 32u) {
+      atomicOr(&bits[wi], (uint32_t)(acc >> (n - 32u)));
+      ++wi;
+      n -= 32u;
+    }
+  };
+  if (__all(P.tmax <= 32u && P.xany == 0u)) {
+    // every pixel of the wave one composed value, no run past 64 pixels
+#pragma unroll
+    for (int q = 0; q < PW_PX; ++q) put(P.v[q], P.tot(q));
+  } else {
+    // entry by entry from the records again (each entry <= 32 bits: longer
+    // ones make the frame FLAG_LONG), then a long run's further digits
+    for (int q = 0; q < PW_PX; ++q) {
+      if ((P.cm >> q) & 1u) {   // coded (P.cm has no bits past the frame's end)
+        const uint32_t r = P.rp[q], run = lane_run(P, q);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const uint2 e = pt_entry(tab, r, i);
+          put(e.x, e.y);
+        }
+        const uint2 e3 = tab.rc[rc_index(run)];
+        put(e3.x, e3.y);
+        if (run > 64u) {
+          for (uint32_t xr = (run - 1u) >> 6;;) {
+            const uint2 d = tab.rc[xr & 7u];
+            put(d.x, d.y);
+            if (xr < 8) break;
+            xr >>= 3;
+          }
+        }
+      }
+    }
+  }
+  if (n) atomicOr(&bits[wi], (uint32_t)(acc << (32u - n)));
+}
+
 __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
   __shared__ PackTab tab;
-  __shared__ uint32_t mask[ENC_TILE / 32];
   __shared__ uint32_t bits[PACK_MAX_WORDS];
   __shared__ uint32_t wsum[PK_THREADS / 64];
   __shared__ uint32_t s_f, s_k;
@@ -1886,8 +2052,6 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
   const uint32_t nt = a.tile_hi - a.tile_lo;
   const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;   // groups per frame
   const uint32_t T = a.tiles_per_frame;
-  const int64_t N = (int64_t)a.W * a.H;
-  const int p0 = 4 * tid;
   const bool lookback_mode = a.pack_mode == 0;
   const uint32_t I = a.pack_slots, slot = blockIdx.x % a.pack_slots;
   uint32_t cf = NONE, ck = 0, seq = 0;   // wave 0's work cursor
@@ -1915,52 +2079,29 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
       cur_f = f;
     }
     for (uint32_t i = tid; i < used_words; i += PK_THREADS) bits[i] = 0;
-    uint32_t rc[4], rn[4];
-    quad_fetch(a, f, tt0, p0, rc);
-    uint32_t gbits = 0;   // the group's bits so far (block-uniform)
-    bool over = false;
-    for (uint32_t s = 0; s < nsub; ++s) {
-      const uint32_t tt = tt0 + s;
-      const int64_t start = (int64_t)tt * ENC_TILE;
-      const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
-      if (s + 1 < nsub) quad_fetch(a, f, tt + 1, p0, rn);
-      TileQuad Q;
-      quad_mask(rc, lane, wid, mask, Q);
-      __syncthreads();
-      PROF_MARK(0);
-      QuadCodes C;
-      quad_codes(tab, mask, start, count, p0, a.tile_next[(uint64_t)f * T + tt], Q, C);
-      const uint32_t x = wave_incl_scan(C.nb);
-      if (lane == 63) wsum[wid] = x;
-      __syncthreads();
-      uint32_t wbase = 0, sbits = 0;
-#pragma unroll
-      for (int i = 0; i < PK_THREADS / 64; ++i) {
-        const uint32_t ws = wsum[i];
-        wbase += (i < wid) ? ws : 0u;
-        sbits += ws;
-      }
-      PROF_MARK(1);
-      over = over || gbits + sbits > a.pack_cap_bits;
-      if (!over && C.nb) {
-        // at bit pp, MSB-first: one 64-bit shift places the bits across
-        // words pp >> 5 and pp >> 5 + 1, both OR-ed into LDS (words shared
-        // with neighbouring lanes)
-        uint32_t pp = gbits + wbase + x - C.nb;
-        quad_emit(tab, Q, C, [&](uint32_t val, uint32_t n) {
-          const uint32_t sh = pp & 31u, wd = pp >> 5;
-          const uint64_t v = (uint64_t)val << ((64u - sh - n) & 63u);
-          atomicOr(&bits[wd], (uint32_t)(v >> 32));
-          atomicOr(&bits[wd + 1], (uint32_t)v);
-          pp += n;
-        });
-      }
-      PROF_MARK(2);
-      gbits += sbits;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rc[q] = rn[q];
-      __syncthreads();   // wsum and mask are rewritten by the next tile
+    __syncthreads();   // the frame's tables in LDS, the buffer clear
+    PROF_MARK(0);
+    // wave wid: tile tt0 + wid of the group
+    LanePx P;
+    uint32_t x = 0;
+    const bool mine = (uint32_t)wid < nsub;   // wave-uniform
+    if (mine) {
+      lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, P);
+      x = wave_incl_scan(P.nb);
     }
+    if (lane == 63) wsum[wid] = mine ? x : 0u;
+    __syncthreads();
+    uint32_t wbase = 0, gbits = 0;   // bits before this wave's tile, the group's bits
+#pragma unroll
+    for (int i = 0; i < PK_THREADS / 64; ++i) {
+      const uint32_t ws = wsum[i];
+      wbase += (i < wid) ? ws : 0u;
+      gbits += ws;
+    }
+    PROF_MARK(1);
+    const bool over = gbits > a.pack_cap_bits;   // block-uniform
+    if (!over && mine && P.nb) lane_emit(tab, P, bits, wbase + x - P.nb);
+    PROF_MARK(2);
     if (wid == 0 && lookback_mode) {
       const unsigned long long off = lookback(a.status, f * ng + g, g, a.band ? a.band_bit0 : a.seed_bit[f], gbits, lane);
       if (lane == 0) s_off = off;
@@ -1990,7 +2131,77 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
           else out32[w0 + m] = __builtin_bswap32(v);
         }
       }
-    } else {
+    } else if (tid == 0) {
+      // over the LDS buffer: listed for enc_pack_over (after this kernel, before enc_edges)
+      const uint32_t k = atomicAdd(a.over_count, 1u);
+      a.over_list[k] = make_uint2(f * ng + g, gbits);
+    }
+    if (lookback_mode && tid == 0) {
+      a.tile_off[t0] = s0;
+      if (over || !(nw && sh)) a.tile_bits[t0] = 0u;
+      if (tt0 + nsub == T) a.data_end[f] = e0;
+    }
+    used_words = over ? 0u : nw + 1;   // an over-cap group writes nothing into the buffer   // an over-cap group writes nothing into the buffer
+    PROF_MARK(4);
+    // the next group: claimed only now, when this block can start it at once
+    // (a group claimed earlier would keep the look-backs of the groups after
+    // it waiting while its block finishes this one)
+    if (wid == 0) {
+      pack_next(a, ng, I, slot, cf, ck, seq, lane);
+      if (lane == 0) { s_f = cf; s_k = ck; }
+    }
+    __syncthreads();
+    f = s_f;
+    g = s_k;
+    PROF_MARK(5);
+#ifdef NICE_PACK_PROF
+    ++pn;
+#endif
+  }
+#ifdef NICE_PACK_PROF
+  if (tid == 0 && (blockIdx.x % 256) == 0)
+    printf("enc_pack block %u: groups %lld cycles/group: wait+mask %lld codes+scan %lld puts %lld lookback %lld "
+           "place %lld claim %lld\n", blockIdx.x, pn, pr[0] / max(pn, 1ll), pr[1] / max(pn, 1ll),
+           pr[2] / max(pn, 1ll), pr[3] / max(pn, 1ll), pr[4] / max(pn, 1ll), pr[5] / max(pn, 1ll));
+#endif
+}
+
+// Groups over enc_pack's LDS buffer (pack_cap_bits: over 32 bits per pixel on
+// average), listed by enc_pack with their bit counts, once every group's
+// offset is published: the words whose first bit is the group's are zeroed,
+// then each code is OR-ed into place tile by tile (the word holding the
+// group's first bit through tile_bits, for enc_edges).  Rare; kept out of
+// enc_pack, whose registers it would otherwise take.
+__global__ __launch_bounds__(PK_THREADS) void enc_pack_over(EncArgs a) {
+  __shared__ PackTab tab;
+  __shared__ uint32_t mask[ENC_TILE / 32];
+  __shared__ uint32_t wsum[PK_THREADS / 64];
+  const uint32_t n_over = *a.over_count;
+  if (blockIdx.x >= n_over) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t nt = a.tile_hi - a.tile_lo;
+  const uint32_t ng = (nt + PACK_SUB - 1) / PACK_SUB;
+  const uint32_t T = a.tiles_per_frame;
+  const int64_t N = (int64_t)a.W * a.H;
+  const int p0 = 4 * tid;
+  const bool lookback_mode = a.pack_mode == 0;
+  uint32_t rc[4];
+  for (uint32_t item = blockIdx.x; item < n_over; item += gridDim.x) {
+    const uint2 it = a.over_list[item];
+    const uint32_t f = it.x / ng, g = it.x % ng, gbits = it.y;
+    const uint32_t k0 = g * PACK_SUB, nsub = min((uint32_t)PACK_SUB, nt - k0);
+    const uint32_t tt0 = a.tile_lo + k0;
+    const uint64_t t0 = (uint64_t)f * T + tt0;
+    __syncthreads();   // the previous item's readers of tab
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(a.packtab + (uint64_t)f * sizeof(PackTab));
+      uint4* dst = reinterpret_cast<uint4*>(&tab);
+      for (int i = tid; i < (int)(sizeof(PackTab) / 16); i += PK_THREADS) dst[i] = src[i];
+    }
+    const unsigned long long s0 = a.tile_off[t0], e0 = s0 + gbits;
+    const uint32_t sh = (uint32_t)(s0 & 31);
+    const uint64_t w0 = s0 >> 5;
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out + (uint64_t)f * a.out_stride);
       // zero the words only this group writes (look-back: every word whose
       // first bit is the group's; bands: the interior ones, enc_tilescan
       // zeroed the partial ones), then OR each code into place, tile by tile
@@ -2040,37 +2251,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
         run += sbits;
         __syncthreads();
       }
-    }
-    if (lookback_mode && tid == 0) {
-      a.tile_off[t0] = s0;
-      if (!over && !(nw && sh)) a.tile_bits[t0] = 0u;
-      if (tt0 + nsub == T) a.data_end[f] = e0;
-    }
-    // an over-cap group has OR-ed its first tiles into the buffer before it
-    // went over: the next group clears all of it
-    used_words = over ? (uint32_t)PACK_MAX_WORDS : nw + 1;
-    PROF_MARK(4);
-    // the next group: claimed only now, when this block can start it at once
-    // (a group claimed earlier would keep the look-backs of the groups after
-    // it waiting while its block finishes this one)
-    if (wid == 0) {
-      pack_next(a, ng, I, slot, cf, ck, seq, lane);
-      if (lane == 0) { s_f = cf; s_k = ck; }
-    }
-    __syncthreads();
-    f = s_f;
-    g = s_k;
-    PROF_MARK(5);
-#ifdef NICE_PACK_PROF
-    ++pn;
-#endif
   }
-#ifdef NICE_PACK_PROF
-  if (tid == 0 && (blockIdx.x % 256) == 0)
-    printf("enc_pack block %u: groups %lld cycles/group: wait+mask %lld codes+scan %lld puts %lld lookback %lld "
-           "place %lld claim %lld\n", blockIdx.x, pn, pr[0] / max(pn, 1ll), pr[1] / max(pn, 1ll),
-           pr[2] / max(pn, 1ll), pr[3] / max(pn, 1ll), pr[4] / max(pn, 1ll), pr[5] / max(pn, 1ll));
-#endif
 }
 
 // Each group's bits in the word holding its first bit (pack_mode 0), OR-ed

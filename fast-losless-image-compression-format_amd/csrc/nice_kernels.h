@@ -74,6 +74,9 @@ struct EncArgs {
   // NICE_ENC_PACK_CAP=b lowers it to b bits per pixel, so tests reach the
   // over-cap path on ordinary frames)
   uint32_t pack_cap_bits;
+  // groups over that buffer, for enc_pack_over: {frame * groups + group, bits}
+  uint32_t* over_count;      // zeroed per launch
+  uint2* over_list;          // n_frames * ceil((tile_hi - tile_lo) / PACK_SUB)
 };
 constexpr uint32_t ENC_GROUP_TILES = 8192;
 
@@ -86,6 +89,10 @@ constexpr uint32_t STRIP_W_HOST = 2048;          // == STRIP_W (nice_encode.hip)
 // the 16K-pixel ring holds 3W + 3 pixels of references plus two tiles (the one
 // being classified and the next one being staged): 3W + 3 + 2048 <= 16384
 constexpr uint32_t CLS_RING_MAX_W = 4777;
+// enc_classify_ring2 / ring2_3: the same with a 32K-pixel ring: 3W + 3 + 2048 <= 32768
+__global__ void enc_classify_ring2(EncArgs a);
+__global__ void enc_classify_ring2_3(EncArgs a);
+constexpr uint32_t CLS_RING2_MAX_W = 10239;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
 constexpr uint32_t DEC_PARSE_THREADS = 512;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring
@@ -99,6 +106,8 @@ __global__ void enc_tilescan(EncArgs a);
 __global__ void enc_group_reduce(EncArgs a, int what);
 __global__ void enc_packtab(EncArgs a);
 __global__ void enc_pack(EncArgs a);
+__global__ void enc_pack_over(EncArgs a);
+constexpr uint32_t PACK_OVER_BLOCKS = 64;   // enc_pack_over's grid (blocks loop over the listed groups)
 __global__ void enc_edges(EncArgs a);
 constexpr uint32_t PACK_BLOCKS_PER_CU = 4;   // enc_pack: 256 threads, ~35 KB LDS
 constexpr int PACK_SUB = 4;                  // tiles per enc_pack work item (group)

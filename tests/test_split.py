@@ -121,16 +121,17 @@ def _split_stats(nice, ctx):
     return nf.value, nr.value
 
 
-def _decode_dev(nice, O, px, w, h, c, ctx, stream=None):
+def _decode_dev(nice, O, px, w, h, c, ctx, stream=None, stream_bytes=None):
     import torch
-    s = O.encode(px, w, h, c)
+    s = stream_bytes if stream_bytes is not None else O.encode(px, w, h, c)
     sb = torch.zeros((1, (len(s) + 255) // 256 * 256), dtype=torch.uint8)
     sb[0, :len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
     sb = sb.cuda()
     lens = torch.tensor([len(s)], dtype=torch.int64, device="cuda")
     dec = torch.zeros((1, w * h * 4), dtype=torch.uint8, device="cuda")
     status = torch.zeros(1, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
+    if stream is not None:   # the inputs are ready before `stream` runs (no device-wide sync)
+        stream.wait_stream(torch.cuda.current_stream())
     nice.decode_batch(sb, lens, w, h, 4, dec, status, flags=nice.DEC_ALPHA_FILL_FF | nice.DEC_TOLERANT_HEADER,
                       stream=stream, ctx=ctx)
     return dec, status
@@ -160,27 +161,39 @@ def test_split_not_coresident_falls_back(nice, O):
     import torch
     w, h, c = 16384, 64, 4
     px = O.gen_syn_v1(w, h, c, 22)
+    s = O.encode(px, w, h, c)
     ctx = nice.Context(0)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     L = nice.lib()
     L.nice_test_occupy.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 5
     busy = torch.cuda.Stream()
     work = torch.cuda.Stream()
+    sb = torch.zeros((1, (len(s) + 255) // 256 * 256), dtype=torch.uint8)
+    sb[0, :len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
+    sb = sb.cuda()
+    lens = torch.tensor([len(s)], dtype=torch.int64, device="cuda")
+    dec = torch.zeros((1, w * h * 4), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    flags = nice.DEC_ALPHA_FILL_FF | nice.DEC_TOLERANT_HEADER
+    # first decode: sizes the context's scratch (no allocation -- which could
+    # synchronise the device -- in the timed one)
+    nice.decode_batch(sb, lens, w, h, 4, dec, status, flags=flags, stream=work, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0 and _split_stats(nice, ctx) == (1, 0)
+    dec.zero_()
     torch.cuda.synchronize()
     # one block per CU (96 KB of LDS each: no 82 KB strip block fits beside it);
     # one CU frees after 20 ms, the rest after 1.5 s
     assert L.nice_test_occupy(ctypes.c_void_p(busy.cuda_stream), cus, 1, 20000, 1500000, 96 * 1024) == 0
     t0 = time.time()
-    dec, status = _decode_dev(nice, O, px, w, h, c, ctx, stream=work)
-    torch.cuda.synchronize()
+    nice.decode_batch(sb, lens, w, h, 4, dec, status, flags=flags, stream=work, ctx=ctx)
+    work.synchronize()
     dt = time.time() - t0
+    torch.cuda.synchronize()
     assert int(status[0]) == 0
     assert np.array_equal(dec[0].view(-1, 4)[:, :3].cpu().numpy(), px.reshape(-1, 4)[:, :3])
     nf, nr = _split_stats(nice, ctx)
-    assert nf == 1
     print(f"decode beside the occupying kernel: {dt:.2f} s, frames redone: {nr}")
-    # the same context decodes normally afterwards (split, no fallback)
-    dec, status = _decode_dev(nice, O, px, w, h, c, ctx)
-    torch.cuda.synchronize()
-    assert int(status[0]) == 0
-    assert _split_stats(nice, ctx) == (1, 0)
+    assert nf == 1
+    assert dt < 1.4, "the decode did not run beside the occupying kernel"
+    assert nr == 1
