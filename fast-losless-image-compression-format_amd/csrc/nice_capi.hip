@@ -308,10 +308,12 @@ static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, u
 // wherever the rows fit it, the strip kernel for wider RGBA rows of whole
 // tiles, the round-1 window kernel otherwise.  `aligned`: the pixel base
 // (frames: and stride) is 4-byte aligned, as the ring and strip loads need.
-enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP };
+enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR };
 static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
   if (w < 3) return CLS_K_TINY;
   if (!aligned || getenv("NICE_ENC_NO_RING")) return CLS_K_WINDOW;
+  static const bool no_pair = getenv("NICE_ENC_NO_PAIR") != nullptr;   // A/B: one tile per iteration
+  if (channels == 4 && w <= CLS_PAIR_MAX_W && !no_pair) return CLS_K_PAIR;
   if (w <= CLS_RING_MAX_W) return CLS_K_RING;
   if (channels == 4 && w % ENC_TILE == 0) return CLS_K_STRIP;
   if (w <= CLS_RING2_MAX_W) return CLS_K_RING2;
@@ -321,11 +323,11 @@ static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
 // strip kernel walks per frame.
 static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work, uint32_t rows_total,
                             hipStream_t st) {
-  const bool ringk = k == CLS_K_RING || k == CLS_K_RING2;
+  const bool ringk = k == CLS_K_RING || k == CLS_K_RING2 || k == CLS_K_PAIR;
   // contiguous tile chunks per block: keeps rows-above reuse in L2 and flushes
   // each block's LDS histogram once per frame; ring kernels: >= 16 tiles per
   // block (the 3-row prefill amortised), 2 blocks per CU (ring2: 1)
-  uint64_t blocks = k == CLS_K_RING ? 2ull * ctx->cus : k == CLS_K_RING2 ? (uint64_t)ctx->cus : 2048;
+  uint64_t blocks = (k == CLS_K_RING || k == CLS_K_PAIR) ? 2ull * ctx->cus : k == CLS_K_RING2 ? (uint64_t)ctx->cus : 2048;
   uint64_t per = (work + blocks - 1) / blocks;
   if (per < (ringk ? 16u : 1u)) per = ringk ? 16 : 1;
   if (ringk && per > 16384) per = 16384;   // its 16-bit per-thread prefix counters
@@ -342,6 +344,9 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
     case CLS_K_RING:
       if (rgb) hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       else hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      break;
+    case CLS_K_PAIR:
+      hipLaunchKernelGGL(enc_classify_pair, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_RING2:
       if (rgb) hipLaunchKernelGGL(enc_classify_ring2_3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
@@ -1179,7 +1184,7 @@ int nice_test_occupy(void* stream, uint32_t blocks, uint32_t short_blocks, uint3
   return NICE_OK;
 }
 // The classify kernel the context's last encode (or band classify) used:
-// 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip.
+// 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip, 5 pair (two tiles per iteration).
 int nice_test_last_classify(nice_ctx* ctx) { return ctx ? ctx->last_classify : -1; }
 
 // Frames of the context's last split decode that went to the fallback launch

@@ -841,6 +841,225 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
   }
   flush(cur_frame);
 }
+// ---------------------------------------------------------------------------
+// K1p: the ring classify with up to two tiles per iteration ("pairs": 4
+// pixels per thread, one staging barrier and one mask barrier per 2048
+// pixels).  The pair is two consecutive tiles of one frame -- one contiguous
+// 2048-pixel range of the raster -- so staging, coded flags and the mode
+// decision run over it as one, with the per-tile outputs (first / last coded
+// pixel, in-tile run digits) per tile; a tile left alone at a frame end or at
+// the end of the block's range takes a one-tile iteration.  The next
+// iteration's pixels load during this one (two tiles of work ahead).  The
+// ring holds 3W + 3 pixels behind the pair plus the pair and the next one:
+// 3W + 3 + 4096 <= RING.
+// ---------------------------------------------------------------------------
+template <int C, int RING>
+__device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
+  constexpr int PQ = 2 * CLS_PPT;   // pixel slots per thread (4)
+  __shared__ uint32_t ring[RING + CLS_GUARD];
+  __shared__ uint32_t stage[C == 3 ? 2 * RGB_TILE_DW + 4 : 1];
+  __shared__ uint32_t hs[C0_N + 2 * SX_N];     // slot histogram (nice_rec.hpp)
+  __shared__ uint32_t run_hist[8];             // run digits (prefixes 5..12)
+  __shared__ uint32_t mask[2 * ENC_TILE / 32];
+  __shared__ uint32_t ltab[2][PQ][16];         // [iteration parity][q][luma reference]: ring index for thread 0
+  const uint64_t total_work = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
+  const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
+  const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
+  if (w_begin >= w_end) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t cbr = (C0_BR << 3) | rec2_abs((uint32_t)lane), csd = (C0_SD << 3) | rec2_abs((uint32_t)lane);
+  const uint32_t cunc = rec2_unc((uint32_t)lane);
+  const uint32_t lback = tid < 16 * PQ && (tid & 15) < 11
+                             ? (uint32_t)lr_rows(tid & 15) * a.W + (uint32_t)lr_px(tid & 15) : 0u;
+  const uint32_t W = a.W;
+  const int64_t N = (int64_t)W * a.H;
+  for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+  if (tid < 8) run_hist[tid] = 0;
+  auto flush = [&](uint32_t frame) {
+    __syncthreads();
+    for (int b = tid; b < N_BINS; b += CLS_THREADS) {
+      uint32_t v = slot_hist_bin(hs, b);
+      if (b >= BIN_PREFIX + P_RUN1 && b < BIN_PREFIX + P_RUN1 + 8) v += run_hist[b - BIN_PREFIX - P_RUN1];
+      if (v) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], v);
+    }
+    __syncthreads();
+    for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+    if (tid < 8) run_hist[tid] = 0;
+  };
+  TileIter it(a, w_begin);
+  uint32_t cur_frame = it.f;
+  {   // prefill: the 3 rows + 3 pixels before the first tile
+    const int64_t start = (int64_t)it.tt() * ENC_TILE;
+    const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
+    const uint8_t* fr = a.px + (uint64_t)cur_frame * a.frame_stride;
+    for (int64_t j = lo + tid; j < start; j += CLS_THREADS) {
+      const uint32_t k = (uint32_t)j & (RING - 1), y = y_from_rgba(px_word<C>(fr, j));
+      ring[k] = y;
+      if (k < CLS_GUARD) ring[RING + k] = y;
+    }
+  }
+  // tiles in the iteration starting at work item w (iterator ti): two when
+  // the next one is in the same frame and in the block's range
+  auto tiles_at = [&](const TileIter& ti, uint64_t w) -> int {
+    return (w + 1 < w_end && ti.k + 1 < ti.nt) ? 2 : 1;
+  };
+  uint32_t pf[PQ];
+  auto fetch = [&](const TileIter& ti, int nti) {
+    const uint32_t f = ti.f;
+    const int64_t start = (int64_t)ti.tt() * ENC_TILE;
+    if (C == 4) {
+      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        const int64_t j = start + q * CLS_THREADS + tid;
+        pf[q] = (q < 2 * nti && j < N) ? fr[j] : 0u;
+      }
+    } else {   // the iteration's dwords tid, 512 + tid, 1024 + tid
+      const uint8_t* fr = a.px + (uint64_t)f * a.frame_stride;
+      const uint64_t j0 = (uint64_t)ti.tt() * RGB_TILE_DW, nbytes = (uint64_t)N * 3;
+      const uint32_t ndw = (uint32_t)nti * RGB_TILE_DW;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const uint32_t d = (uint32_t)(q * CLS_THREADS + tid);
+        pf[q] = d < ndw && 4 * (j0 + d) < nbytes ? rgb_dword(fr, nbytes, j0 + d) : 0u;
+      }
+    }
+  };
+  uint64_t w = w_begin;
+  int nti = tiles_at(it, w);
+  fetch(it, nti);
+  uint32_t par = 0;
+  while (w < w_end) {
+    const int cur = nti;
+    const uint32_t f = it.f;
+    const uint32_t tt = it.tt();
+    if (f != cur_frame) {
+      flush(cur_frame);
+      cur_frame = f;
+    }
+    const int64_t start = (int64_t)tt * ENC_TILE;
+    const int count = (int)min((int64_t)(cur * ENC_TILE), N - start);   // pixels of the iteration
+    // stage the iteration's pixels (Y space)
+    uint32_t pxw[PQ];
+    if (C == 4) {
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) pxw[q] = pf[q];
+    } else {   // bytes via LDS: the previous iteration's readers are past its staging barrier
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if ((uint32_t)(q * CLS_THREADS + tid) < (uint32_t)cur * RGB_TILE_DW) stage[q * CLS_THREADS + tid] = pf[q];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        const uint32_t b = 3u * (uint32_t)(q * CLS_THREADS + tid);
+        pxw[q] = q < 2 * cur ? __builtin_amdgcn_alignbit(stage[(b >> 2) + 1], stage[b >> 2], (b & 3u) * 8u) : 0u;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      if (q < 2 * cur) {
+        const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1), y = y_from_rgba(pxw[q]);
+        ring[k] = y;
+        if (k < CLS_GUARD) ring[RING + k] = y;
+      }
+    }
+    if (tid < 16 * PQ)
+      ltab[par][tid >> 4][tid & 15] = ((uint32_t)(start + (tid >> 4) * CLS_THREADS) - lback) & (RING - 1);
+    // the next iteration's pixels, in flight during this one
+    TileIter nx = it;
+    nx.step((uint32_t)cur);
+    if (w + cur < w_end) {
+      nti = tiles_at(nx, w + cur);
+      fetch(nx, nti);
+    }
+    __syncthreads();
+    // coded flags -> bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
+    uint32_t coded_bits = 0;
+    unsigned long long wbal[PQ];
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const int64_t i = start + p;
+      const uint32_t* bl = ring + ((uint32_t)(start + q * CLS_THREADS - 1) & (RING - 1)) + tid;
+      const bool coded = q < 2 * cur && p < count && (i == 0 || bl[1] != bl[0]);
+      const unsigned long long bal = __ballot(coded);
+      wbal[q] = bal;
+      if (lane == 0 && q < 2 * cur) {
+        const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
+        mask[wb] = (uint32_t)bal;
+        mask[wb + 1] = (uint32_t)(bal >> 32);
+      }
+      coded_bits |= (coded ? 1u : 0u) << q;
+    }
+    __syncthreads();
+    if (tid < 64 * cur) {   // wave j: first / last coded pixel of tile j
+      const int j = tid >> 6;
+      const uint32_t* mk = mask + 32 * j;
+      const uint32_t mw = lane < ENC_TILE / 32 ? mk[lane] : 0u;
+      const unsigned long long nz = __ballot(mw != 0);
+      if (lane == 0) {
+        const uint64_t t = it.tile() + (uint64_t)j;
+        const int64_t sj = start + (int64_t)j * ENC_TILE;
+        uint32_t first = NONE, last = NONE;
+        if (nz) {
+          const int fw = __builtin_ctzll(nz), lw = 63 - __builtin_clzll(nz);
+          first = (uint32_t)(sj + fw * 32 + __builtin_ctz(mk[fw]));
+          last = (uint32_t)(sj + lw * 32 + 31 - __builtin_clz(mk[lw]));
+        }
+        a.tile_first[t] = first;
+        a.tile_last[t] = last;
+      }
+    }
+    const bool fast = start >= 3 * (int64_t)W + 3;
+    uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
+    uint32_t rec[PQ];
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {   // every pixel's mode first (independent LDS reads)
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      uint32_t rf = cunc;
+      if (q < 2 * cur) {   // block-uniform
+        if (fast)
+          rf = classify_ring<false, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u,
+                                          ltab[par][q], cbr, csd);
+        else
+          rf = classify_ring<true, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W,
+                                         (uint32_t)(start + p), nullptr, cbr, csd);
+      }
+      rec[q] = coded ? rf : cunc;
+    }
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      if (q >= 2 * cur) continue;   // block-uniform
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      if (p < count) recs[p] = rec[q];
+      slot_hist_add(hs, rec[q]);
+      // a run follows only if the next pixel is uncoded; runs crossing the
+      // tile's end are enc_tailruns' (lane 63's next pixel is in the next wave)
+      const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
+      if (coded && !next_coded) {
+        const int j = q >> 1, pl = p - j * ENC_TILE;   // tile and index in it
+        const int cj = min(count - j * ENC_TILE, ENC_TILE);
+        const unsigned long long above = lane < 63 ? (wbal[q] >> (lane + 1)) : 0ull;
+        const int nxl = above ? pl + 1 + (int)__builtin_ctzll(above) : next_coded_local(mask + 32 * j, pl | 63);
+        if (nxl < cj && nxl > pl + 1) {
+          uint32_t mm = (uint32_t)(nxl - pl - 2);
+          while (true) {
+            atomicAdd(&run_hist[mm & 7u], 1u);
+            if (mm < 8) break;
+            mm >>= 3;
+          }
+        }
+      }
+    }
+    par ^= 1u;
+    it.step((uint32_t)cur);
+    w += (uint64_t)cur;
+  }
+  flush(cur_frame);
+}
+
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4, CLS_RING>(a); }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3, CLS_RING>(a); }
 // a 32K-pixel ring (128 KB, one block per CU) for rows of up to
@@ -848,6 +1067,10 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { e
 // 1024 != 0, e.g. 7680 for 8K UHD) and RGB frames
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2(EncArgs a) { enc_classify_ring_body<4, 2 * CLS_RING>(a); }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_3(EncArgs a) { enc_classify_ring_body<3, 2 * CLS_RING>(a); }
+// pairs of tiles per iteration (16K ring: W <= CLS_PAIR_MAX_W)
+// (RGBA; an RGB pair's 6 KB byte stage would push the block past 80 KB of LDS,
+// one block per CU)
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_pair(EncArgs a) { enc_classify_pair_body<4, CLS_RING>(a); }
 
 // ---------------------------------------------------------------------------
 // K1s: classify, strip-staged (RGBA frames with W % 1024 == 0 too wide for the

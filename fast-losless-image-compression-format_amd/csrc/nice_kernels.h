@@ -93,6 +93,9 @@ constexpr uint32_t CLS_RING_MAX_W = 4777;
 __global__ void enc_classify_ring2(EncArgs a);
 __global__ void enc_classify_ring2_3(EncArgs a);
 constexpr uint32_t CLS_RING2_MAX_W = 10239;
+// enc_classify_pair: RGBA, two tiles per iteration, 16K ring: 3W + 3 + 4096 <= 16384
+__global__ void enc_classify_pair(EncArgs a);
+constexpr uint32_t CLS_PAIR_MAX_W = 4095;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
 constexpr uint32_t DEC_PARSE_THREADS = 512;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring

@@ -11,7 +11,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-WINDOW, TINY, RING, RING2, STRIP = range(5)
+WINDOW, TINY, RING, RING2, STRIP, PAIR = range(6)
 
 
 def _same(got, want, what):
@@ -40,6 +40,7 @@ def _encode_dev(nice, px, w, h, c, ctx):
 
 @pytest.mark.parametrize("shape,kind", [((7680, 64, 4), RING2), ((6000, 32, 3), RING2), ((10239, 9, 4), RING2),
                                         ((10239, 11, 3), RING2), ((4777, 20, 4), RING), ((4778, 20, 3), RING2),
+                                        ((4095, 20, 4), PAIR), ((4095, 20, 3), RING), ((1000, 30, 4), PAIR),
                                         ((8192, 12, 4), STRIP), ((10240, 5, 3), WINDOW), ((11000, 5, 4), WINDOW)],
                          ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
 def test_route_and_bitexact(nice, O, shape, kind):
@@ -68,7 +69,7 @@ def test_8k_uhd_batch(nice, O):
         _same(bytes(out[i, :int(lens[i])].cpu().numpy()), O.encode(frames[i], w, h, c), i)
 
 
-@pytest.mark.parametrize("shape,kind", [((1920, 1080, 4, 4), RING), ((1000, 700, 3, 3), RING),
+@pytest.mark.parametrize("shape,kind", [((1920, 1080, 4, 4), PAIR), ((1000, 700, 3, 3), RING),
                                         ((7680, 300, 4, 3), RING2), ((8192, 200, 4, 2), STRIP)],
                          ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
 def test_band_routes(nice, O, shape, kind):
