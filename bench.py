@@ -141,7 +141,7 @@ def max_over_ranks(value, dist, device):
 
 
 # timing phase -> the kernels that implement it (first match in the PMC summary)
-PHASE_KERNELS = {"enc_classify": ["enc_classify_ring", "enc_classify"],
+PHASE_KERNELS = {"enc_classify": ["enc_classify_pair", "enc_classify_ring", "enc_classify"],
                  "enc_tilebits": ["enc_tilebits_hist", "enc_tilebits"],
                  "dec_reconstruct": ["dec_rows", "dec_rows_wide", "dec_reconstruct"]}
 
@@ -151,7 +151,10 @@ def load_traffic(phase, frames, path=None):
     summary (bytes per frame from separate FETCH_SIZE / WRITE_SIZE passes,
     gfx950-corrected; see profiles/README.md), scaled to this launch's frame
     count; None if absent."""
-    path = path or os.path.join(ROOT, "profiles", "pmc_traffic_r03d.json")
+    if path is None:   # the newest committed summary (profiles/pmc_traffic_rNN*.json)
+        import glob
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_r*.json")))
+        path = cands[-1] if cands else os.path.join(ROOT, "profiles", "pmc_traffic_r03d.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -159,8 +162,8 @@ def load_traffic(phase, frames, path=None):
         return None
     for k in PHASE_KERNELS.get(phase, [phase]):
         if k in d.get("kernels", {}):
-            return int(d["kernels"][k]["hbm_bytes_per_frame"] * frames)
-    return None
+            return int(d["kernels"][k]["hbm_bytes_per_frame"] * frames), os.path.basename(path)
+    return None, None
 
 
 def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
@@ -640,7 +643,7 @@ def main():
         "dec_reconstruct": out_px_bytes,
     }
     dom = max((k for k in phase if k in algo), key=lambda k: phase[k]["ms_total"])
-    traffic = load_traffic(dom, F)
+    traffic, traffic_src = load_traffic(dom, F)
     avg_s = phase[dom]["ms_total"] / 1e3 / phase[dom]["launches"]
     achieved = algo[dom] / avg_s / 1e9
     total_px = N * F * args.steps * world
@@ -669,6 +672,7 @@ def main():
                      "frac": round(achieved * 1e9 / HBM_PEAK, 5),
                      "traffic": traffic,
                      "traffic_ratio": round(traffic / algo[dom], 3) if traffic else None,
+                     "traffic_source": traffic_src,
                      "algo_bytes_per_launch": algo[dom],
                      "avg_launch_ms": round(avg_s * 1e3, 4)},
         # whole path against HBM: encode (px in + stream out) + decode (stream in + px out)

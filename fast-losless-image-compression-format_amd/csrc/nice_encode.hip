@@ -517,22 +517,27 @@ struct RingAcc {   // classify<false> accessor: RGB spread of pixel i - (rows*W 
 // The four neighbour groups of the lane's pixel: b0 = pixels i-3 .. i (row y),
 // b1 = row y-1 from 3 left, b2 = pixel i-2W, b3 = row y-3 from 3 left; the
 // hit's difference is read again at rbase[ltab[k] + tid].
+// X: the lane's own pixel (Y space), from the caller's registers where it
+// staged it (saves one ring read per pixel).
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
                                                const uint32_t* b3, const uint32_t* rbase, uint32_t tid, uint32_t W,
-                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd);
+                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd,
+                                               uint32_t X);
 template <bool HEAD, int RING = CLS_RING>
 __device__ __forceinline__ uint32_t classify_ring(const uint32_t* ring, uint32_t s, uint32_t tid, uint32_t W,
-                                                  uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
+                                                  uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd,
+                                                  uint32_t X) {
   return classify_y<HEAD>(ring + ((s - 3u) & (RING - 1)) + tid, ring + ((s - W - 3u) & (RING - 1)) + tid,
                           ring + ((s - 2u * W) & (RING - 1)) + tid,
-                          ring + ((s - 3u * W - 3u) & (RING - 1)) + tid, ring, tid, W, i, ltab, cbr, csd);
+                          ring + ((s - 3u * W - 3u) & (RING - 1)) + tid, ring, tid, W, i, ltab, cbr, csd, X);
 }
 template <bool HEAD>
 __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_t* b1, const uint32_t* b2,
                                                const uint32_t* b3, const uint32_t* rbase, uint32_t tid, uint32_t W,
-                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd) {
-  const uint32_t X = b0[3], L2 = b0[1], L3 = b0[0];
+                                               uint32_t i, const uint32_t* ltab, uint32_t cbr, uint32_t csd,
+                                               uint32_t X) {
+  const uint32_t L2 = b0[1], L3 = b0[0];
   uint32_t L = b0[2];
   const uint32_t U = b1[3], UR1 = b1[4], UR3 = b1[6], UL3 = b1[0];
   const uint32_t U2 = b2[0];
@@ -742,9 +747,11 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
         pxw[q] = __builtin_amdgcn_alignbit(stage[(b >> 2) + 1], stage[b >> 2], (b & 3u) * 8u);
       }
     }
+    uint32_t yv[CLS_PPT];   // the thread's pixels in Y space (classify's X)
 #pragma unroll
     for (int q = 0; q < CLS_PPT; ++q) {
       const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1), y = y_from_rgba(pxw[q]);
+      yv[q] = y;
       ring[k] = y;
       if (k < CLS_GUARD) ring[RING + k] = y;
     }
@@ -800,10 +807,10 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
       uint32_t rf;
       if (fast)   // block-uniform: both variants are straight-line code
         rf = classify_ring<false, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u, ltab[w & 1][q],
-                                  cbr, csd);
+                                        cbr, csd, yv[q]);
       else
         rf = classify_ring<true, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, (uint32_t)(start + p),
-                                 nullptr, cbr, csd);
+                                       nullptr, cbr, csd, yv[q]);
       rec[q] = coded ? rf : cunc;
     }
 #pragma unroll
@@ -955,12 +962,14 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
         pxw[q] = q < 2 * cur ? __builtin_amdgcn_alignbit(stage[(b >> 2) + 1], stage[b >> 2], (b & 3u) * 8u) : 0u;
       }
     }
+    uint32_t yv[PQ];   // the thread's pixels in Y space (classify's X)
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
+      yv[q] = y_from_rgba(pxw[q]);
       if (q < 2 * cur) {
-        const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1), y = y_from_rgba(pxw[q]);
-        ring[k] = y;
-        if (k < CLS_GUARD) ring[RING + k] = y;
+        const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1);
+        ring[k] = yv[q];
+        if (k < CLS_GUARD) ring[RING + k] = yv[q];
       }
     }
     if (tid < 16 * PQ)
@@ -1021,10 +1030,10 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
       if (q < 2 * cur) {   // block-uniform
         if (fast)
           rf = classify_ring<false, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W, 0u,
-                                          ltab[par][q], cbr, csd);
+                                          ltab[par][q], cbr, csd, yv[q]);
         else
           rf = classify_ring<true, RING>(ring, (uint32_t)(start + q * CLS_THREADS), (uint32_t)tid, W,
-                                         (uint32_t)(start + p), nullptr, cbr, csd);
+                                         (uint32_t)(start + p), nullptr, cbr, csd, yv[q]);
       }
       rec[q] = coded ? rf : cunc;
     }
@@ -1215,10 +1224,10 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
         const uint32_t* b3 = win[(y - 3) & 3] + cs + tid;
         uint32_t rf;
         if (fast)
-          rf = classify_y<false>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, 0u, ltab[j][q], cbr, csd);
+          rf = classify_y<false>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, 0u, ltab[j][q], cbr, csd, b0[3]);
         else
           rf = classify_y<true>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, (uint32_t)(start + p), ltab[j][q], cbr,
-                                csd);
+                                csd, b0[3]);
         rec[q] = coded ? rf : cunc;
       }
 #pragma unroll
