@@ -383,6 +383,12 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     st = p.decode(o_list, lens, d_list)
     t_dec = time.perf_counter() - t1
     assert st == [0] * n
+    # the timed frames, checked outside the timed regions: every frame's stream
+    # length equals its distinct source's (all n encodes, not only the warm-up),
+    # and each decode buffer -- last written by the timed run -- holds its source
+    assert all(lens[i] == lens[i % k] for i in range(n)), "streamed: timed stream lengths differ"
+    for i in range(k):
+        assert torch.equal(dec[i].view(N, 4)[:, :3], src[i].view(N, 4)[:, :3]), "streamed timed round trip"
     t_enc = max_over_ranks(t_enc, dist, device)
     t_dec = max_over_ranks(t_dec, dist, device)
     p.close()
@@ -393,6 +399,8 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     return {"workload": f"{n * world} x {W}x{H} RGBA frames from pinned host memory, {n} per GPU, "
                         f"H2D/compute/D2H overlapped ({depth} slots x {batch} frames)",
             "host_numa_node": node,
+            "check": f"all {n} timed streams' lengths equal their source's; the {k} decode buffers after the "
+                     f"timed run equal their sources",
             "encode_mpix_s": round(px_all / t_enc / 1e6, 2),
             "decode_mpix_s": round(px_all / t_dec / 1e6, 2),
             "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),

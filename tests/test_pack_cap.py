@@ -71,3 +71,26 @@ def test_pack_noise_row_real_cap(nice, O):
     assert 3 * rare > 40, rare        # a noise pixel: prefix + three rare residuals
     got = nice.encode_bytes(px, w, h, c)
     assert got == want
+
+
+def test_pack_rare_path_mixed(nice, O):
+    """Waves whose pixels mix >32-bit codes (noise in a frame of RGB-mode
+    pixels with geometric residuals) with runs longer than 64 pixels (extra
+    run digits, code.rs:391-406): the packer's entry-by-entry path, next to
+    ordinary waves; the stream must equal the oracle's."""
+    w, h, c = 2048, 256, 4
+    px = O.gen_rgb_field(w, h, c, 3, [40, 41, 200]).reshape(h, w, c)
+    for y in (40, 41, 200):          # noise rows cut by runs of 65..300 pixels
+        x = 17
+        while x < w - 400:
+            n = 65 + (x * 7) % 236
+            px[y, x:x + n, :3] = px[y, x, :3]
+            x += n + 50
+    px[120, 100:1900, :3] = (5, 6, 7)   # one long run in the smooth field
+    px = px.reshape(-1)
+    want, st = O.encode(px, w, h, c, with_stats=True)
+    assert st.max_emitted_aob <= 25
+    got = nice.encode_bytes(px, w, h, c)
+    if got != want:
+        d = next(i for i in range(min(len(got), len(want))) if got[i] != want[i])
+        pytest.fail(f"first differing byte {d} of {len(want)} (got {len(got)})")
