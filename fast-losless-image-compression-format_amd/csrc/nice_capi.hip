@@ -379,7 +379,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   const uint32_t T = tiles_for(w, h);
-  const bool aligned = ((uintptr_t)d_px & 3) == 0 && (frame_stride & 3) == 0;
+  // one frame: its stride is never applied (an odd W*H*3 RGB stride is fine)
+  const bool aligned = ((uintptr_t)d_px & 3) == 0 && (n_frames == 1 || (frame_stride & 3) == 0);
   const ClsKind ck = pick_classify(w, channels, aligned);
   if ((uint64_t)n_frames * T >= (1ull << 32)) return NICE_E_ARG;   // enc_pack's 32-bit work counter
   EncLayout L = enc_layout(n_frames, T, N);
@@ -807,12 +808,14 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     size_t lds = ((size_t)SPLIT_THREADS_HOST * 7 + 4 + 4 * ((size_t)sps * 16 + 6 + ((sps * 16 + 6) >> 4) + 17)) * 4;
     lds = std::max<size_t>(lds, 82 * 1024);
     NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    a.test_absent_strip = getenv("NICE_TEST_SPLIT_ABSENT") ? 1u : 0u;
     for (uint32_t f0 = 0; f0 < n_frames; f0 += split_frames) {
       a.split_f0 = f0;
       hipLaunchKernelGGL(dec_rows_split, dim3(std::min(split_frames, n_frames - f0) * strips),
                          dim3(SPLIT_THREADS_HOST), lds, st, a);
     }
     a.split_f0 = 0;
+    a.test_absent_strip = 0;
     // fallback: frames whose strips timed out waiting for a non-resident
     // neighbour (every other block returns at once)
     DecArgs r = a;

@@ -2106,6 +2106,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
   __shared__ int err;
   const uint32_t k = a.strips;
   const uint32_t f = a.split_f0 + blockIdx.x / k, j = blockIdx.x % k;
+  if (a.test_absent_strip && j == k - 1) return;   // block-uniform (tests only)
   const uint32_t W = a.W, H = a.H;
   const uint32_t nseg = (W + S - 1) / S;
   const uint32_t sps = (nseg + k - 1) / k;

@@ -187,6 +187,9 @@ struct DecArgs {
   // only frames whose strips could not all be resident (hand_abort ==
   // SPLIT_REDO: a wait timed out) are reconstructed, the others return at once
   uint32_t redo;
+  // tests (NICE_TEST_SPLIT_ABSENT): the last strip of every frame returns at
+  // once, as a block that never became resident would, so the others time out
+  uint32_t test_absent_strip;
 };
 constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =

@@ -153,10 +153,12 @@ def test_split_wider_than_16384(nice, O):
 
 
 def test_split_not_coresident_falls_back(nice, O):
-    """A 16384-wide decode while another stream's kernel holds every CU but
-    one for 1.5 s: the strips cannot all be resident, the first one's wait
-    times out, and the frame is reconstructed by the fallback launch -- exact
-    pixels, status 0, no NICE_E_HIP."""
+    """A 16384-wide decode queued while another stream's kernel holds every CU
+    but one for 1.5 s: exact pixels, status 0, no NICE_E_HIP.  Workgroups go
+    to the XCDs round-robin, so strips on XCDs with no free CU (and blocks of
+    the parse kernels) start only when the occupying blocks end; whether the
+    split then ran co-resident or a strip timed out and its frame was redone
+    depends on that order -- both must give the same pixels."""
     import ctypes
     import torch
     w, h, c = 16384, 64, 4
@@ -194,6 +196,25 @@ def test_split_not_coresident_falls_back(nice, O):
     assert np.array_equal(dec[0].view(-1, 4)[:, :3].cpu().numpy(), px.reshape(-1, 4)[:, :3])
     nf, nr = _split_stats(nice, ctx)
     print(f"decode beside the occupying kernel: {dt:.2f} s, frames redone: {nr}")
-    assert nf == 1
-    assert dt < 1.4, "the decode did not run beside the occupying kernel"
-    assert nr == 1
+    assert nf == 1 and nr in (0, 1)
+
+
+@pytest.mark.parametrize("shape", [(16384, 64, 4), (20000, 24, 3)], ids=["16384x64x4", "20000x24x3"])
+def test_split_absent_strip_redone(nice, O, shape, monkeypatch):
+    """A strip that never becomes resident (NICE_TEST_SPLIT_ABSENT: the last
+    strip of each frame returns at entry): its neighbour's halo wait times out
+    (0.2 s), the frame's strips stop, and the fallback launch (dec_rows_wide;
+    dec_reconstruct above 16384 columns) reconstructs the frame exactly."""
+    import torch
+    monkeypatch.setenv("NICE_TEST_SPLIT_ABSENT", "1")
+    w, h, c = shape
+    px = O.gen_syn_v1(w, h, c, 23)
+    ctx = nice.Context(0)
+    t0 = time.time()
+    dec, status = _decode_dev(nice, O, px, w, h, c, ctx)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    assert int(status[0]) == 0
+    assert np.array_equal(dec[0].view(-1, 4)[:, :3].cpu().numpy(), px.reshape(-1, c)[:, :3])
+    assert _split_stats(nice, ctx) == (1, 1)
+    assert dt < 5.0, dt
