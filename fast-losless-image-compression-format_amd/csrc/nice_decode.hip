@@ -1689,7 +1689,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   const uint32_t RS = rows_ring_stride(W);
   uint32_t* ring = (LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * RS)) + ROWS_RB;
   // per-row class table (S == 16), double-buffered by row parity: x = kind bits
-  // | pixels back + 3, y = ring offset of the referenced row's pixel 0 plus 3
+  // | 8 for a row-above class | pixels back + 3, y = ring offset of the referenced row's pixel 0 plus 3
   // minus pixels back, so a reference's word is 17 * lane + p + y (+ a +-1
   // padding correction for the first and last three pixels of a segment)
   __shared__ uint2 rtab[2][16];
@@ -1698,7 +1698,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const uint32_t c = threadIdx.x;
       const unsigned long long kinds = yy == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
       const uint32_t rows = (CLS_ROWS_PACK >> (2 * c)) & 3u, dxp3 = (uint32_t)(CLS_PX_PACK >> (3 * c)) & 7u;
-      rtab[yy & 1u][c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3,
+      rtab[yy & 1u][c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3 | (c >= 4u ? 8u : 0u),
                                     ((yy - rows) & (ROWS_RING - 1)) * RS + 3u - dxp3);
     }
   };
@@ -1767,16 +1767,23 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         if (p < 3 || p > S - 4) ad += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
         const uint32_t o = ring[ad + p];
         const uint32_t c = spread3(r & 0xFFFFFFu);
-        w[p] = (e.x & 0xF0000000u) | (((cls >= 4u ? o : 0u) + c) & SP_K);
+        // a row-above class (bit 3 of the entry) adds the referenced pixel: a
+        // VALU mask instead of a compare into an SGPR pair per pixel
+        w[p] = (e.x & 0xF0000000u) | (((o & wmask(e.x, 3)) + c) & SP_K);
       }
-      if (lane == nseg - 1) {   // references past the row end into row y itself: pixels 0..2
+      // references past the row end into row y itself (pixels 0..2): only
+      // columns W-3 .. W-1 have them -- the last segment, and the one before
+      // it when the last holds fewer than three pixels (W % 16 in {1, 2}).
+      // Branch-free (per-pixel branches held exec masks in SGPRs, which
+      // spilled), and only the wave holding those lanes runs it.
+      if (x0 + S + 2u >= W) {
 #pragma unroll
         for (int p = 0; p < S; ++p) {
-          const uint32_t r = rec_canon(rn[p], a.rec_tag);
+          const uint32_t r = rec_canon(rn[p], a.rec_tag);   // padding: a run record (class 1)
           const uint32_t cls = r >> 24;
-          const uint32_t tx = x0 + p + 3u - (tb[cls].x & 7u);
-          if (cls >= 4u && ((CLS_ROWS_PACK >> (2 * cls)) & 3u) == 1u && tx >= W && p < nvalid)
-            w[p] = W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8);
+          const uint32_t tx = x0 + p + 3u - ((uint32_t)(CLS_PX_PACK >> (3u * cls)) & 7u);
+          const bool cur = cls >= 4u && ((CLS_ROWS_PACK >> (2u * cls)) & 3u) == 1u && tx >= W;
+          w[p] = cur ? (W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8)) : w[p];
         }
       }
     } else {
@@ -1863,9 +1870,14 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       ++n_fix;
       if (lane == 0) pend[(rd + 1) & 1u] = 0;
       if (!cur_done) {   // pixels 0..2 of the row are exact now (lane 0)
+        if (x0 + S + 2u >= W) {   // the lanes that can hold W_CUR words (above)
+          const uint32_t h0 = head3[0], h1 = head3[1], h2 = head3[2];
 #pragma unroll
-        for (int p = 0; p < S; ++p) {
-          if (w[p] & W_CUR) w[p] = (head3[(w[p] >> 8) & 3u] + (w[p] & SP_K)) & SP_K;
+          for (int p = 0; p < S; ++p) {
+            const uint32_t k = (w[p] >> 8) & 3u;
+            const uint32_t hv = k == 0u ? h0 : k == 1u ? h1 : h2;
+            w[p] = (w[p] & W_CUR) ? ((hv + (w[p] & SP_K)) & SP_K) : w[p];
+          }
         }
         cur_done = true;
       }
@@ -1881,6 +1893,13 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       // anything in one round and forced its whole wave onto the interval
       // chain; the leftmost unfinished lane always has an exact left tail
       const bool go = !fin && exact_in;
+#ifndef NICE_ROWS_HOIST
+      // the words as opaque per round: otherwise the compiler hoists the select
+      // masks of all 16 pixels out of the round loop, and their SGPR pairs
+      // spill to VGPR lanes (a writelane per mask per row, a readlane per use)
+#pragma unroll
+      for (int p = 0; p < S; ++p) asm volatile("" : "+v"(w[p]));
+#endif
       lu = rows_chain_exact<S>(v, r0, r1, r2, w, prev, lu, go);
       if (go) {
         if (lu >= 0) atomicCAS(err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs

@@ -135,7 +135,7 @@ constexpr uint32_t DEC_CK_BITS = 1024;      // sync checkpoint spacing inside a 
                                             // 128: +30 % dec_sync -- scattered stores)
 constexpr uint32_t DEC_MIN_CHUNK_BITS = 1024;   // speculative-parse slice: a power of two
 constexpr uint32_t DEC_MAX_CHUNK_BITS = 16384;  // chosen per call (nice_capi.hip)
-constexpr uint32_t DEC_PLACE_WAVES = 4;          // dec_place: one wave per slice (2 or 8 per block: slower)
+constexpr uint32_t DEC_PLACE_WAVES = 4;          // dec_place: one wave per slice (2 or 8 per block: slower; several slices per wave, their bookkeeping loads batched: slower too)
 constexpr uint32_t DEC_EMIT_BITS = 1024;        // record-emission sub-slice (<= the slice)
 constexpr int DEC_MAX_SEGS = 64;            // one lane per row segment
 
