@@ -1689,7 +1689,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   const uint32_t RS = rows_ring_stride(W);
   uint32_t* ring = (LDS_RING ? (sm + nthr * 7 + 8) : (a.rowbuf + (uint64_t)f * ROWS_RING * RS)) + ROWS_RB;
   // per-row class table (S == 16), double-buffered by row parity: x = kind bits
-  // | 8 for a row-above class | pixels back + 3, y = ring offset of the referenced row's pixel 0 plus 3
+  // | pixels back + 3, y = ring offset of the referenced row's pixel 0 plus 3
   // minus pixels back, so a reference's word is 17 * lane + p + y (+ a +-1
   // padding correction for the first and last three pixels of a segment)
   __shared__ uint2 rtab[2][16];
@@ -1698,7 +1698,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       const uint32_t c = threadIdx.x;
       const unsigned long long kinds = yy == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
       const uint32_t rows = (CLS_ROWS_PACK >> (2 * c)) & 3u, dxp3 = (uint32_t)(CLS_PX_PACK >> (3 * c)) & 7u;
-      rtab[yy & 1u][c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3 | (c >= 4u ? 8u : 0u),
+      rtab[yy & 1u][c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3,
                                     ((yy - rows) & (ROWS_RING - 1)) * RS + 3u - dxp3);
     }
   };
@@ -1767,9 +1767,8 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         if (p < 3 || p > S - 4) ad += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
         const uint32_t o = ring[ad + p];
         const uint32_t c = spread3(r & 0xFFFFFFu);
-        // a row-above class (bit 3 of the entry) adds the referenced pixel: a
-        // VALU mask instead of a compare into an SGPR pair per pixel
-        w[p] = (e.x & 0xF0000000u) | (((o & wmask(e.x, 3)) + c) & SP_K);
+        // (a VALU mask from a table bit instead of the compare: 4 % slower)
+        w[p] = (e.x & 0xF0000000u) | (((cls >= 4u ? o : 0u) + c) & SP_K);
       }
       // references past the row end into row y itself (pixels 0..2): only
       // columns W-3 .. W-1 have them -- the last segment, and the one before
