@@ -1991,13 +1991,14 @@ __device__ __forceinline__ unsigned long long st_load(const unsigned long long* 
 // `base`), publishes its own end; returns the tile's start bit.  w: the tile's
 // status index; k: the tiles before it in its frame.  Every tile waited on
 // was claimed earlier by a running block, which never waits on a later one.
+// agg_out: the count was published already (ST_AGG).
 __device__ unsigned long long lookback(unsigned long long* st, uint32_t w, uint32_t k, unsigned long long base,
-                                       uint32_t bits, int lane) {
+                                       uint32_t bits, int lane, bool agg_out = false) {
   if (k == 0) {
     if (lane == 0) st_store(&st[w], ST_INCL | (base + bits));
     return base;
   }
-  if (lane == 0) st_store(&st[w], ST_AGG | bits);
+  if (lane == 0 && !agg_out) st_store(&st[w], ST_AGG | bits);
   unsigned long long excl = 0;
   uint32_t j = w - 1, rem = k;
   while (true) {
@@ -2201,24 +2202,30 @@ __device__ __forceinline__ uint32_t rc_index(uint32_t run) {
 // The lane's 16 pixels of tile tt of frame f: each pixel's composed code and
 // length, the lane's bit count.  Pixel indices are < 2^30 (the boundary's
 // frame cap): 32-bit arithmetic.
-__device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab, uint32_t f, uint32_t tt,
-                                           uint32_t next_tile_px, int lane, LanePx& P) {
+// The lane's 16 records of tile tt of frame f (issued early: enc_pack loads the
+// next group's records while it places the current one).
+__device__ __forceinline__ void lane_recs(const EncArgs& a, uint32_t f, uint32_t tt, int lane, uint32_t (&rec)[PW_PX]) {
   const int64_t N = (int64_t)a.W * a.H;
   const int64_t start = (int64_t)tt * ENC_TILE;
   const int count = (int)((N - start) < ENC_TILE ? (N - start) : ENC_TILE);
   const int p0 = PW_PX * lane;
-  P.rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
-  uint32_t rec[PW_PX];
+  const uint32_t* rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
   if (p0 + PW_PX <= count) {
 #pragma unroll
     for (int q = 0; q < PW_PX / 4; ++q) {
-      const uint4 r = reinterpret_cast<const uint4*>(P.rp)[q];
+      const uint4 r = reinterpret_cast<const uint4*>(rp)[q];
       rec[4 * q] = r.x; rec[4 * q + 1] = r.y; rec[4 * q + 2] = r.z; rec[4 * q + 3] = r.w;
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < PW_PX; ++q) rec[q] = (p0 + q < count) ? P.rp[q] : rec2_unc(0);
+    for (int q = 0; q < PW_PX; ++q) rec[q] = (p0 + q < count) ? rp[q] : rec2_unc(0);
   }
+}
+__device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab, uint32_t f, uint32_t tt,
+                                           uint32_t next_tile_px, int lane, const uint32_t (&rec)[PW_PX], LanePx& P) {
+  const int64_t start = (int64_t)tt * ENC_TILE;
+  const int p0 = PW_PX * lane;
+  P.rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
   P.cm = 0;
 #pragma unroll
   for (int q = 0; q < PW_PX; ++q) P.cm |= (rec2_coded(rec[q]) ? 1u : 0u) << q;
@@ -2337,6 +2344,8 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
   __syncthreads();
   uint32_t f = s_f, g = s_k;
   uint32_t cur_f = NONE, used_words = PACK_MAX_WORDS;
+  uint32_t rec[PW_PX];    // the wave's tile records (prefetched during the previous group)
+  bool have_rec = false;
   while (f != NONE) {
     const uint32_t k0 = g * PACK_SUB, nsub = min((uint32_t)PACK_SUB, nt - k0);
     const uint32_t tt0 = a.tile_lo + k0;
@@ -2355,7 +2364,8 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     uint32_t x = 0;
     const bool mine = (uint32_t)wid < nsub;   // wave-uniform
     if (mine) {
-      lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, P);
+      if (!have_rec) lane_recs(a, f, tt0 + wid, lane, rec);
+      lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, rec, P);
       x = wave_incl_scan(P.nb);
     }
     if (lane == 63) wsum[wid] = mine ? x : 0u;
@@ -2369,14 +2379,43 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     }
     PROF_MARK(1);
     const bool over = gbits > a.pack_cap_bits;   // block-uniform
+#ifndef NICE_PACK_LATE_AGG
+    // the group's count goes out before the puts: the look-backs of the
+    // groups after it wait on it (a look-back was ~40 % of a group's time)
+    const bool agg_out = lookback_mode && g > 0;
+    if (agg_out && tid == 0) st_store(&a.status[f * ng + g], ST_AGG | gbits);
+#else
+    const bool agg_out = false;
+#endif
     if (!over && mine && P.nb) lane_emit(tab, P, bits, wbase + x - P.nb);
     PROF_MARK(2);
     if (wid == 0 && lookback_mode) {
-      const unsigned long long off = lookback(a.status, f * ng + g, g, a.band ? a.band_bit0 : a.seed_bit[f], gbits, lane);
+      const unsigned long long off = lookback(a.status, f * ng + g, g, a.band ? a.band_bit0 : a.seed_bit[f], gbits, lane,
+                                              agg_out);
       if (lane == 0) s_off = off;
     }
+#ifdef NICE_PACK_PREFETCH
+    // (A/B, off: 4.30 -> 4.51 ms per 256 frames) the next group claimed once
+    // this one's offset is published, its records loading while this one is
+    // placed
+    if (wid == 0) {
+      pack_next(a, ng, I, slot, cf, ck, seq, lane);
+      if (lane == 0) { s_f = cf; s_k = ck; }
+    }
+#endif
     __syncthreads();
     PROF_MARK(3);
+#ifdef NICE_PACK_PREFETCH
+    const uint32_t nf = s_f, nk = s_k;
+    have_rec = false;
+    if (nf != NONE) {
+      const uint32_t nsub2 = min((uint32_t)PACK_SUB, nt - nk * PACK_SUB);
+      if ((uint32_t)wid < nsub2) {
+        lane_recs(a, nf, a.tile_lo + nk * PACK_SUB + wid, lane, rec);
+        have_rec = true;
+      }
+    }
+#endif
     // place the group's bits at its stream offset
     const unsigned long long s0 = lookback_mode ? s_off : a.tile_off[t0], e0 = s0 + gbits;
     const uint32_t sh = (uint32_t)(s0 & 31);
@@ -2412,6 +2451,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     }
     used_words = over ? 0u : nw + 1;   // an over-cap group writes nothing into the buffer   // an over-cap group writes nothing into the buffer
     PROF_MARK(4);
+#ifndef NICE_PACK_PREFETCH
     // the next group: claimed only now, when this block can start it at once
     // (a group claimed earlier would keep the look-backs of the groups after
     // it waiting while its block finishes this one)
@@ -2422,6 +2462,11 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     __syncthreads();
     f = s_f;
     g = s_k;
+#else
+    __syncthreads();   // the buffer's readers are done before the next clear
+    f = nf;
+    g = nk;
+#endif
     PROF_MARK(5);
 #ifdef NICE_PACK_PROF
     ++pn;
