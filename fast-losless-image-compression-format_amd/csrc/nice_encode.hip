@@ -299,14 +299,7 @@ __device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col, ui
   const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins; skipped when no lane needs it
   uint32_t lk = 11u, lt = 0u;
-#ifdef NICE_CLS_LUMA_VOTE
   const bool need_luma = __any(!br && !sd && !l2);
-#else
-  // straight-line (no vote): a wave-level branch per pixel slot kept the
-  // caller's pixel slots from interleaving (each slot's luma block waited
-  // behind the vote of its own LDS reads)
-  const bool need_luma = !HEAD || __any(!br && !sd && !l2);
-#endif
   if (need_luma) {
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
 #pragma unroll
@@ -579,14 +572,9 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
   const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins (code.rs:293-339)
   uint32_t lk = 11u, lt = 0u;
-#ifdef NICE_CLS_LUMA_VOTE
+  // (A/B: the search made unconditional on the fast path -- more VALU per
+  // pixel -- was 6 % slower at 512 frames: whole waves often skip it)
   const bool need_luma = __any(!br && !sd && !l2);
-#else
-  // straight-line (no vote): a wave-level branch per pixel slot kept the
-  // caller's pixel slots from interleaving (each slot's luma block waited
-  // behind the vote of its own LDS reads)
-  const bool need_luma = !HEAD || __any(!br && !sd && !l2);
-#endif
   if (need_luma) {
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
     if constexpr (HEAD) {
@@ -627,18 +615,7 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
                             : ((C0_LUMA << 3) | (SX_LUMA << 14) | (SX_LUMA << 23)) + (lk << 9);
   const uint32_t rec_lu = lbase + (__builtin_amdgcn_ubfe(lf, 10, 6) << 3) + ((lf & 0x1Fu) << 14) +
                           ((lf & (0x1Fu << 20)) << 3);
-#ifndef NICE_CLS_BRANCHY
-  // every candidate opaque: otherwise the compiler sinks the luma tests into
-  // divergent branches on br / sd (an exec save / restore and a skip test per
-  // pixel slot), which also kept the slots from interleaving
-  uint32_t rec_l = (l2 || lk < 11u) ? rec_lu : rec_rgb;
-  asm volatile("" : "+v"(rec_l));
-  uint32_t rec_nb = sd ? rec_sd : rec_l;
-  asm volatile("" : "+v"(rec_nb));
-  return br ? rec_br : rec_nb;
-#else
   return br ? rec_br : sd ? rec_sd : (l2 || lk < 11u) ? rec_lu : rec_rgb;
-#endif
 }
 
 // slot histogram (nice_rec.hpp) add of one record: three unconditional LDS
