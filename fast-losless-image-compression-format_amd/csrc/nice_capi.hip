@@ -851,6 +851,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
             "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
             "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
             h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
+    fprintf(stderr, "[nice dec stats] unknown segment tails: copies of an unknown %llu, narrowed %llu\n", h[24], h[25]);
     fprintf(stderr, "[nice dec stats] re-parse met previous parse at checkpoint:");
     for (int k = 0; k < 17; ++k) fprintf(stderr, " %d:%llu", k, h[32 + k]);
     fprintf(stderr, "\n");

@@ -1850,6 +1850,13 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       atomicAdd(&stats[1], 1ull);
       atomicAdd(&stats[3], (unsigned long long)(lu + 1));
       if (lu >= S - 3) atomicAdd(&stats[2], 1ull);
+      // unknown tails: every tail pixel a full-width interval (a copy chain
+      // from the unknown entry or a current-row reference) or some narrowed one
+      const uint32_t tl0 = v[S - 1].len, tl1 = v[S - 2].len, tl2 = v[S - 3].len;
+      if (tl0 | tl1 | tl2) {
+        const bool copies = (tl0 == 0u || tl0 == SP_K) && (tl1 == 0u || tl1 == SP_K) && (tl2 == 0u || tl2 == SP_K);
+        atomicAdd(&stats[copies ? 24 : 25], 1ull);
+      }
     }
     rows_barrier<LDS_RING>();
     const unsigned long long c2 = stats ? __builtin_amdgcn_s_memtime() : 0;
