@@ -74,22 +74,44 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_UNSUPPORTED);
     return;
   }
-  BitSrc src{s, len};
+#ifdef NICE_PROF_DTABLES
+  long long tp[10];
+  int tpn = 0;
+#define DT_MARK() do { if (tpn < 10) tp[tpn++] = clock64(); } while (0)
+#else
+#define DT_MARK() do {} while (0)
+#endif
+  DT_MARK();
+  // the file and table headers (770 bytes) staged in LDS as big-endian words
+  // with one load per thread (the fields were ~12 dependent global reads per
+  // thread: most of this kernel's time for a single frame)
+  constexpr int HDR_WORDS = (FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS + 31) / 32 + 2;
+  __shared__ uint32_t hw[HDR_WORDS];
+  {
+    const BitSrc src{s, len};
+    for (int i = threadIdx.x; i < HDR_WORDS; i += 256) hw[i] = src.peek32((uint64_t)i * 32u);
+  }
+  __syncthreads();
+  auto hpeek = [&](uint32_t pos) -> uint32_t {   // 32 bits at header bit pos, MSB first
+    const uint32_t wi = pos >> 5, o = pos & 31u;
+    return (uint32_t)((((unsigned long long)hw[wi] << 32 | hw[wi + 1]) << o) >> 32);
+  };
   // Decoder side field widths are fixed: a 5-bit max (<= 31) always selects
   // 7-bit length fields (hfe.rs:177-178).
   for (int st = threadIdx.x; st < N_STREAMS; st += 256) {
     uint32_t pos = FILE_HEADER_BYTES * 8;
     for (int q = 0; q < st; ++q) pos += 5 + 7 * stream_size(q);
-    smax[st] = (uint8_t)(src.peek32(pos) >> 27);
+    smax[st] = (uint8_t)(hpeek(pos) >> 27);
   }
-  for (int st = 0; st < N_STREAMS; ++st) {
-    uint32_t pos = FILE_HEADER_BYTES * 8;
+  for (int i = threadIdx.x; i < N_BINS; i += 256) {
+    int st = 0;
+    while (st + 1 < N_STREAMS && i >= stream_base(st + 1)) ++st;
+    uint32_t pos = FILE_HEADER_BYTES * 8 + 5;
     for (int q = 0; q < st; ++q) pos += 5 + 7 * stream_size(q);
-    pos += 5;
-    for (int i = threadIdx.x; i < stream_size(st); i += 256)
-      lens[stream_base(st) + i] = (uint8_t)(src.peek32(pos + 7u * i) >> 25);
+    lens[i] = (uint8_t)(hpeek(pos + 7u * (uint32_t)(i - stream_base(st))) >> 25);
   }
   __syncthreads();
+  DT_MARK();
   const bool tolerant = (a.flags & NICE_DEC_TOLERANT_HEADER) && !(a.flags & NICE_DEC_STRICT_REFERENCE);
   if (tolerant) {
     // Spilled max fields (oracle tolerant_tables): a max above 31
@@ -129,35 +151,49 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
       for (int i = 0; i < n && ok; ++i) kraft += (unsigned __int128)1 << (mx - lens[b + i]);
       if (!ok || kraft != ((unsigned __int128)1 << mx)) atomicOr(&bad, 1);
     }
-  } else if (threadIdx.x < N_STREAMS) {
-    // validity: every length in [1, max], max attained, Kraft sum == 1
-    const int st = threadIdx.x;
-    const uint32_t mx = smax[st];
-    uint64_t kraft = 0;
-    uint32_t seen = 0;
-    bool ok = mx >= 1 && mx <= 31;
-    for (int i = 0; i < stream_size(st) && ok; ++i) {
-      const uint32_t l = lens[stream_base(st) + i];
-      if (l < 1 || l > mx) ok = false;
-      else { kraft += 1ull << (mx - l); seen = max(seen, l); }
+  } else {
+    // validity: every length in [1, max], max attained, Kraft sum == 1 -- every
+    // symbol at once, per-stream sums by LDS atomics (a lane per stream looping
+    // over its symbols took ~0.13 ms of a single frame's decode)
+    __shared__ unsigned long long vkraft[N_STREAMS];
+    __shared__ uint32_t vseen[N_STREAMS];
+    if (threadIdx.x < N_STREAMS) { vkraft[threadIdx.x] = 0; vseen[threadIdx.x] = 0; }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N_BINS; i += 256) {
+      int st = 0;
+#pragma unroll
+      for (int q = 1; q < N_STREAMS; ++q) st += i >= stream_base(q) ? 1 : 0;
+      const uint32_t mx = smax[st], l = lens[i];
+      if (l < 1 || l > mx || mx > 31) atomicOr(&bad, 1);
+      else {
+        atomicAdd(&vkraft[st], 1ull << (mx - l));
+        atomicMax(&vseen[st], l);
+      }
     }
-    if (!ok || seen != mx || kraft != (1ull << mx)) atomicOr(&bad, 1);
-    // strict: a max length above 24 lets the reference refill loop wrap its u8
-    // bit offset and spin forever (bitreader.rs:88-97): outside its domain
-    if ((a.flags & NICE_DEC_STRICT_REFERENCE) && mx > 24) atomicOr(&bad, 1);
+    __syncthreads();
+    if (threadIdx.x < N_STREAMS) {
+      const int st = threadIdx.x;
+      const uint32_t mx = smax[st];
+      if (mx < 1 || vseen[st] != mx || vkraft[st] != (1ull << mx)) atomicOr(&bad, 1);
+      // strict: a max length above 24 lets the reference refill loop wrap its u8
+      // bit offset and spin forever (bitreader.rs:88-97): outside its domain
+      if ((a.flags & NICE_DEC_STRICT_REFERENCE) && mx > 24) atomicOr(&bad, 1);
+    }
   }
   __syncthreads();
   if (bad) {
     if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_UNSUPPORTED);
     return;
   }
+  DT_MARK();
   // canonical order per stream: rank by (len desc, symbol desc)
   for (int st = 0; st < N_STREAMS; ++st) {
     const int n = stream_size(st), b = stream_base(st);
     for (int i = threadIdx.x; i < n; i += 256) {
       const uint8_t li = lens[b + i];
       int rank = 0;
-      for (int j = 0; j < n; ++j) {
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) {   // independent reads: unrolled, batched
         const uint8_t lj = lens[b + j];
         rank += (lj > li) || (lj == li && j > i);
       }
@@ -165,6 +201,7 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     }
   }
   __syncthreads();
+  DT_MARK();
   __shared__ uint8_t lbits[N_STREAMS];
   __shared__ uint16_t loff[N_STREAMS];
   if (threadIdx.x == 0) {
@@ -185,9 +222,19 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     for (int st = 0; st < N_STREAMS; ++st) { loff[st] = (uint16_t)o; o += 1u << lbits[st]; }
   }
   __syncthreads();
-  // canonical codes (hfe.rs:271-290): one lane per stream, serial in LDS
+  DT_MARK();
+  // canonical codes (hfe.rs:271-290): one lane per stream, serial in LDS; the
+  // lengths in rank order first (all threads), so the serial loop reads one
+  // independent word per symbol instead of a dependent order -> length chain
   __shared__ uint32_t clo[N_BINS];
   __shared__ uint8_t clen[N_BINS];
+  for (int i = threadIdx.x; i < N_BINS; i += 256) {
+    int st = 0;
+#pragma unroll
+    for (int q = 1; q < N_STREAMS; ++q) st += i >= stream_base(q) ? 1 : 0;
+    clen[i] = lens[stream_base(st) + order[i]];
+  }
+  __syncthreads();
   if (threadIdx.x < N_STREAMS) {
     const int st = threadIdx.x;
     const int n = stream_size(st), b = stream_base(st);
@@ -203,14 +250,13 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     uint32_t prev = 0;
     uint64_t prev_lo = ~0ull;
     bool ok = true;
+#pragma unroll 4
     for (int k = 0; k < n; ++k) {
-      const int sym = order[b + k];
-      const uint32_t l = lens[b + sym];
+      const uint32_t l = clen[b + k];
       if (l < prev) cur >>= (prev - l) & 63u;
       if (prev > 0) cur += 1;
       const unsigned long long code64 = (1ull << (l & 63u)) - cur - 1ull;
       prev = l;
-      clen[b + k] = (uint8_t)l;
       if (l > mx) { clo[b + k] = 0xFFFFFFFFu; continue; }
       const uint64_t lo = (uint64_t)(uint32_t)code64 << (mx - l);
       if ((code64 >> l) != 0 || (prev_lo != ~0ull && lo + (1ull << (mx - l)) > prev_lo)) ok = false;
@@ -224,6 +270,7 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_UNSUPPORTED);
     return;
   }
+  DT_MARK();
   for (int i = threadIdx.x; i < N_BINS; i += 256) {
     T->lo[i] = clo[i];
     T->sym[i] = order[i];
@@ -234,13 +281,15 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
   // canonical order (lower bounds descending) with lo <= x -- a complete,
   // non-overlapping code (checked above) covers every x exactly once.  A code
   // longer than the width leaves the long-code marker 0.
+  DT_MARK();
   const uint32_t n_lut = (uint32_t)loff[N_STREAMS - 1] + (1u << lbits[N_STREAMS - 1]);
   __shared__ int lut_hole;
   if (threadIdx.x == 0) lut_hole = 0;
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < n_lut; e += 256) {
     int st = 0;
-    while (st + 1 < N_STREAMS && e >= loff[st + 1]) ++st;
+#pragma unroll
+    for (int q = 1; q < N_STREAMS; ++q) st += e >= loff[q] ? 1 : 0;   // independent reads, no search loop
     const uint32_t lb = lbits[st], mx = smax[st];
     const uint32_t x = (e - loff[st]) << (mx - lb);
     int lo = stream_base(st), hi = lo + stream_size(st) - 1;
@@ -263,6 +312,12 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
     T->fast = (!lut_hole && smax[S_PREFIX] + m_pay <= 64u) ? 1u : 0u;
     a.data_start[f] = FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS;
   }
+#ifdef NICE_PROF_DTABLES
+  DT_MARK();
+  if (threadIdx.x == 0 && f == 0)
+    printf("dec_tables cycles: stage+lens %lld valid %lld rank %lld widths %lld canon %lld copy %lld lut %lld (n=%d)\n",
+           tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5], tp[7] - tp[6], tpn);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -759,10 +814,16 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
   const uint64_t base = (uint64_t)f * a.max_chunks;
   const uint32_t per = (nc + 1023) / 1024;
   const uint32_t c0 = threadIdx.x * per, c1 = min(c0 + per, nc);
+  // a thread's range in batches of 8 independent loads (one at a time, a
+  // single frame's ~85 chunks per thread were ~85 dependent round trips)
+  constexpr uint32_t B = 8;
   unsigned long long sum = 0;
-  for (uint32_t j = c0; j < c1; ++j) {
-    const unsigned long long v = a.chunk_px[base + j];
-    sum = (sum + v < sum) ? ~0ull : sum + v;   // saturate (garbage past the image end)
+  for (uint32_t j0 = c0; j0 < c1; j0 += B) {
+    unsigned long long v[B];
+#pragma unroll
+    for (uint32_t q = 0; q < B; ++q) v[q] = j0 + q < c1 ? a.chunk_px[base + j0 + q] : 0ull;
+#pragma unroll
+    for (uint32_t q = 0; q < B; ++q) sum = (sum + v[q] < sum) ? ~0ull : sum + v[q];   // saturate (garbage past the image end)
   }
   part[threadIdx.x] = sum;
   __syncthreads();
@@ -777,10 +838,15 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
     __syncthreads();
   }
   unsigned long long run = threadIdx.x ? part[threadIdx.x - 1] : 0ull;
-  for (uint32_t j = c0; j < c1; ++j) {
-    a.chunk_start[base + j] = run;
-    const unsigned long long v = a.chunk_px[base + j];
-    run = (run + v < run) ? ~0ull : run + v;
+  for (uint32_t j0 = c0; j0 < c1; j0 += B) {
+    unsigned long long v[B];
+#pragma unroll
+    for (uint32_t q = 0; q < B; ++q) v[q] = j0 + q < c1 ? a.chunk_px[base + j0 + q] : 0ull;
+#pragma unroll
+    for (uint32_t q = 0; q < B; ++q) {
+      if (j0 + q < c1) a.chunk_start[base + j0 + q] = run;
+      run = (run + v[q] < run) ? ~0ull : run + v[q];
+    }
   }
   if (threadIdx.x == 1023) {
     // total must cover the image

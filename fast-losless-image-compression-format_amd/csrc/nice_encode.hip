@@ -2321,8 +2321,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
   __syncthreads();
   uint32_t f = s_f, g = s_k;
   uint32_t cur_f = NONE, used_words = PACK_MAX_WORDS;
-  uint32_t rec[PW_PX];    // the wave's tile records (prefetched during the previous group)
-  bool have_rec = false;
+  uint32_t rec[PW_PX];    // the wave's tile records
   while (f != NONE) {
     const uint32_t k0 = g * PACK_SUB, nsub = min((uint32_t)PACK_SUB, nt - k0);
     const uint32_t tt0 = a.tile_lo + k0;
@@ -2341,7 +2340,7 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     uint32_t x = 0;
     const bool mine = (uint32_t)wid < nsub;   // wave-uniform
     if (mine) {
-      if (!have_rec) lane_recs(a, f, tt0 + wid, lane, rec);
+      lane_recs(a, f, tt0 + wid, lane, rec);
       lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, rec, P);
       x = wave_incl_scan(P.nb);
     }
@@ -2371,28 +2370,8 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
                                               agg_out);
       if (lane == 0) s_off = off;
     }
-#ifdef NICE_PACK_PREFETCH
-    // (A/B, off: 4.30 -> 4.51 ms per 256 frames) the next group claimed once
-    // this one's offset is published, its records loading while this one is
-    // placed
-    if (wid == 0) {
-      pack_next(a, ng, I, slot, cf, ck, seq, lane);
-      if (lane == 0) { s_f = cf; s_k = ck; }
-    }
-#endif
     __syncthreads();
     PROF_MARK(3);
-#ifdef NICE_PACK_PREFETCH
-    const uint32_t nf = s_f, nk = s_k;
-    have_rec = false;
-    if (nf != NONE) {
-      const uint32_t nsub2 = min((uint32_t)PACK_SUB, nt - nk * PACK_SUB);
-      if ((uint32_t)wid < nsub2) {
-        lane_recs(a, nf, a.tile_lo + nk * PACK_SUB + wid, lane, rec);
-        have_rec = true;
-      }
-    }
-#endif
     // place the group's bits at its stream offset
     const unsigned long long s0 = lookback_mode ? s_off : a.tile_off[t0], e0 = s0 + gbits;
     const uint32_t sh = (uint32_t)(s0 & 31);
@@ -2428,10 +2407,11 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     }
     used_words = over ? 0u : nw + 1;   // an over-cap group writes nothing into the buffer   // an over-cap group writes nothing into the buffer
     PROF_MARK(4);
-#ifndef NICE_PACK_PREFETCH
     // the next group: claimed only now, when this block can start it at once
     // (a group claimed earlier would keep the look-backs of the groups after
-    // it waiting while its block finishes this one)
+    // it waiting while its block finishes this one; claiming during the
+    // placement, or loading the next group's records then, measured no
+    // faster: r04e, r04n)
     if (wid == 0) {
       pack_next(a, ng, I, slot, cf, ck, seq, lane);
       if (lane == 0) { s_f = cf; s_k = ck; }
@@ -2439,11 +2419,6 @@ __global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
     __syncthreads();
     f = s_f;
     g = s_k;
-#else
-    __syncthreads();   // the buffer's readers are done before the next clear
-    f = nf;
-    g = nk;
-#endif
     PROF_MARK(5);
 #ifdef NICE_PACK_PROF
     ++pn;
