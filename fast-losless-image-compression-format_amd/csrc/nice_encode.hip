@@ -562,7 +562,11 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
   const uint32_t pred = has_up ? avg3(rgb_from_y(U), lrgb) : lrgb;
   // small diff (code.rs:208-247)
   const uint32_t d = xr + K3(259u) - pred;
-  const bool sd = has_left && ((d & K3(0x3F8u)) == K3(0x100u)) && ((((d & K3(7u)) + K3(1u)) & K3(8u)) == 0);
+  // every field in [256, 262]: bits 3-9 0b0100000 (field in [256, 263]) and
+  // bit 3 of field + 1 clear (field != 263), OR-ed so one compare covers all
+  // three fields (an OR only adds bit 3, which 0x100 lacks; no carry: fields
+  // <= 515)
+  const bool sd = has_left && ((d & K3(0x3F8u)) | ((d + K3(1u)) & K3(8u))) == K3(0x100u);
   const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
   // luma2 against the prediction (code.rs:252-292)
   const uint32_t pg = (pred >> 10) & 0xFFu;
