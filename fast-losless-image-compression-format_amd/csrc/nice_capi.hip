@@ -282,10 +282,10 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.band = 0;
   a.over_count = (uint32_t*)(base + L.o_overn);
   a.over_list = (uint2*)(base + L.o_overl);
-  a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * 32;
+  a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * NICE_PACK_CAP_BPP;
   if (const char* ev = getenv("NICE_ENC_PACK_CAP")) {   // tests: bits per pixel of the LDS buffer
     const int b = atoi(ev);
-    if (b >= 1 && b <= 32) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * (uint32_t)b;
+    if (b >= 1 && b <= NICE_PACK_CAP_BPP) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * (uint32_t)b;
   }
   return a;
 }

@@ -1714,7 +1714,9 @@ __global__ __launch_bounds__(64) void enc_header(EncArgs a) {
 // A thread owns 4 consecutive pixels and reads their records with one 16-byte
 // load.
 // ---------------------------------------------------------------------------
-constexpr int PACK_CAP_BITS = PACK_SUB * ENC_TILE * 32;    // LDS bit buffer: <= 32 bits per pixel
+// LDS bit buffer: <= NICE_PACK_CAP_BPP bits per pixel on average over a group
+// (denser groups go to enc_pack_over)
+constexpr int PACK_CAP_BITS = PACK_SUB * ENC_TILE * NICE_PACK_CAP_BPP;
 constexpr int PACK_MAX_WORDS = PACK_CAP_BITS / 32 + 2;
 constexpr int PK_THREADS = 256;
 
@@ -2299,7 +2301,7 @@ __device__ __forceinline__ void lane_emit(const PackTab& tab, const LanePx& P, u
   if (n) atomicOr(&bits[wi], (uint32_t)(acc << (32u - n)));
 }
 
-__global__ __launch_bounds__(PK_THREADS, 4) void enc_pack(EncArgs a) {
+__global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncArgs a) {
   __shared__ PackTab tab;
   __shared__ uint32_t bits[PACK_MAX_WORDS];
   __shared__ uint32_t wsum[PK_THREADS / 64];

@@ -112,7 +112,13 @@ __global__ void enc_pack(EncArgs a);
 __global__ void enc_pack_over(EncArgs a);
 constexpr uint32_t PACK_OVER_BLOCKS = 64;   // enc_pack_over's grid (blocks loop over the listed groups)
 __global__ void enc_edges(EncArgs a);
-constexpr uint32_t PACK_BLOCKS_PER_CU = 4;   // enc_pack: 256 threads, ~35 KB LDS
+#ifndef NICE_PACK_BPC
+#define NICE_PACK_BPC 4
+#endif
+#ifndef NICE_PACK_CAP_BPP
+#define NICE_PACK_CAP_BPP 32     // enc_pack's LDS group buffer: bits per pixel
+#endif
+constexpr uint32_t PACK_BLOCKS_PER_CU = NICE_PACK_BPC;   // enc_pack: 256 threads, ~35 KB LDS
 constexpr int PACK_SUB = 4;                  // tiles per enc_pack work item (group)
 __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
