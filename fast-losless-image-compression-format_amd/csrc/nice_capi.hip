@@ -618,14 +618,16 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !single_wave;
   const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds + 1024 <= 160 * 1024;   // + static LDS
-  // 8-pixel segments, twice the lanes per frame, where 16-pixel segments
-  // would leave SIMDs of a frame's CU idle (W <= 2048: at most two waves) and
-  // frames do not share CUs: 64 x 1080p 7.83 -> 6.32 ms; slower at 4K (four
-  // waves already: single frame 16.1 -> 17.7 ms).  NICE_DEC_SEG=8/16 forces a size
+  // 8-pixel segments (twice the lanes per frame) only on request
+  // (NICE_DEC_SEG=8): they were the default where 16-pixel segments leave SIMDs
+  // of a frame's CU idle (W <= 2048, frames not sharing CUs: 64 x 1080p 7.83 ->
+  // 6.32 ms in round 2), but the round-3/4 row kernel with 16-pixel segments is
+  // as fast or faster at every width measured (round 4, profiles/r04v, r04y:
+  // 64 x 1080p reconstruct 6.58 vs 6.88 ms, W = 1280 / 1024 / 640: 6.68 / 5.77
+  // / 6.22 vs 6.91 / 6.00 / 6.30 ms)
   const uint32_t rows8_thr = ((w + 7) / 8 + 63) / 64 * 64;
   const size_t rows8_lds = ((size_t)rows8_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;
-  bool rows8 = use_rows && rows_in_lds && rows_thr <= 128 && rows8_thr <= 512 && rows8_lds <= 160 * 1024 &&
-               n_frames <= (uint32_t)ctx->cus;
+  bool rows8 = false;
   if (const char* ev = getenv("NICE_DEC_SEG")) rows8 = atoi(ev) == 8 && use_rows && rows_in_lds &&
                                                        rows8_thr <= 512 && rows8_lds <= 160 * 1024;
   // wide frames, few of them: strips of <= 256 segments on separate CUs

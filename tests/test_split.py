@@ -102,8 +102,8 @@ def test_split_corrupt_stream_fails_fast(nice, O, monkeypatch):
 
 @pytest.mark.parametrize("seg", ["8", "16"])
 def test_row_segment_sizes(nice, O, seg, monkeypatch):
-    """dec_rows8 (8-pixel segments, the default for narrow frames in small
-    batches) and dec_rows (16) forced on the same frames: identical pixels."""
+    """dec_rows8 (8-pixel segments, on request since round 4) and dec_rows (16)
+    forced on the same frames: identical pixels."""
     monkeypatch.setenv("NICE_DEC_SEG", seg)
     monkeypatch.setenv("NICE_DEC_SPLIT", "0")
     for name, px, w, h, c in _cases(O) + [("syn64x9x3", O.gen_syn_v1(64, 9, 3, 2), 64, 9, 3),

@@ -1,5 +1,9 @@
 """Diagnostic: per-kernel instruction audit of the device assembly (spill
-reloads, quarter-rate multiplies, exec-mask branches, scratch, VALU count).
+reloads, quarter-rate multiplies, exec-mask branches, scratch, VALU count),
+and the first vmcnt wait after each outermost loop head ("heads=..."): a
+vmcnt(0) there in a loop that prefetches its next loads means the compiler
+found a path with loads but no counted store behind them, and the wait drains
+the prefetch and the stores ("waits").
 Usage: python tools/isa_audit.py [source.hip ...]"""
 import re, subprocess, sys, os
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -16,6 +20,13 @@ for src in srcs:
         c = lambda pat: len(re.findall(pat, body, re.M))
         pats = {"valu": r"^\s+v_", "salu": r"^\s+s_", "readlane": r"v_readlane_b32", "writelane": r"v_writelane_b32",
                 "mul_lo": r"v_mul_lo_u32|v_mul_hi_u32", "b64": r"v_(lshlrev|lshrrev|ashrrev)_b64|v_cmp_[a-z]+_u64",
-                "saveexec": r"s_and_saveexec", "scratch": r"scratch_|buffer_store|buffer_load", "swappc": r"s_swappc"}
+                "saveexec": r"s_and_saveexec", "scratch": r"scratch_", "swappc": r"s_swappc"}
         counts = " ".join(f"{k}={c(v)}" for k, v in pats.items())
-        print(f"{(name.group(1) if name else k[:30]):22s} {counts}")
+        lines = body.split("\n")
+        heads = []
+        for i, l in enumerate(lines):
+            if "Loop Header: Depth=1" in l:
+                w = next((re.search(r"vmcnt\((\d+)\)", x).group(1) for x in lines[i:i + 40]
+                          if re.search(r"s_waitcnt vmcnt\(\d+\)$", x.strip())), "-")
+                heads.append(w)
+        print(f"{(name.group(1) if name else k[:30]):22s} {counts} heads={','.join(heads) or '-'}")
