@@ -1182,8 +1182,16 @@ constexpr uint32_t CLS_PX_LO = (uint32_t)CLS_PX_PACK, CLS_PX_HI = (uint32_t)(CLS
 __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32_t W, const uint32_t* sdl,
                                                  bool& bad) {
   const uint32_t pfx = ev & 7u;
+#ifndef NICE_PLACE_BRANCHY
+  // prefix tests as bits of one mask: as == compares of one value, the
+  // compiler turned the selects below into a switch of exec-masked branches
+  const uint32_t pm = 1u << pfx;
+  const bool isbr = (pm & (1u << P_BACK_REF)) != 0u, islu = (pm & (1u << P_LUMA)) != 0u;
+  const bool issd = (pm & (1u << P_SMALL_DIFF)) != 0u, isl2 = (pm & (1u << P_LUMA2)) != 0u;
+#else
   const bool isbr = pfx == (uint32_t)P_BACK_REF, islu = pfx == (uint32_t)P_LUMA;
   const bool issd = pfx == (uint32_t)P_SMALL_DIFF, isl2 = pfx == (uint32_t)P_LUMA2;
+#endif
   const uint32_t s0 = (ev >> 3) & 511u, s1 = (ev >> 12) & 255u, s2 = (ev >> 20) & 255u, s3 = (ev >> 7) & 31u;
   const uint32_t s0l = s0 & 15u;   // LUMA: the reference (bits 3..6)
   const uint32_t id = min(isbr ? s0 : 5u + s0l, 15u);
@@ -1199,9 +1207,19 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
   const uint32_t c_sd = sdl[min(s0, 342u)];
   const uint32_t g2 = (s0 - 32u) & 255u;
   const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
-  const uint32_t c_rgb = (s0 & 255u) | (s1 << 8) | (s2 << 16);
+  uint32_t c_rgb = (s0 & 255u) | (s1 << 8) | (s2 << 16);
   bad = (isbr || islu) ? bad_ref : (isl2 && q < W);
+#ifndef NICE_PLACE_BRANCHY
+  // the candidates opaque: otherwise the select chain compiles to a switch of
+  // exec-masked branches on the prefix (about 35 scalar instructions and 8
+  // branches per event, every prefix present in most waves)
+  uint32_t c_br = (cls << 24) | (islu ? c_lu : 0u);
+  uint32_t c_sd2 = c_sd, c_l22 = c_l2;
+  asm volatile("" : "+v"(c_br), "+v"(c_sd2), "+v"(c_l22), "+v"(c_rgb));
+  return (isbr || islu) ? c_br : issd ? c_sd2 : isl2 ? c_l22 : c_rgb;
+#else
   return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+#endif
 }
 
 __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
