@@ -1176,11 +1176,14 @@ __global__ __launch_bounds__(1024) void dec_heads(DecArgs a) {
 // a run past N or a reference the reference rejects sets NICE_E_FORMAT.
 // ---------------------------------------------------------------------------
 // make_record for dec_place: 32-bit arithmetic (q <= N <= 2^30, 3W < 2^32),
-// the SMALL_DIFF constant from a table (sdl: 343 packed constants in LDS).
+// the SMALL_DIFF constant from a table (sdl: 343 packed constants in LDS), the
+// reference's class and offset from another (idt: 16 entries per block).
+#ifdef NICE_PLACE_ARITH
 constexpr uint32_t ID_CLS_LO = (uint32_t)ID_CLS_PACK, ID_CLS_HI = (uint32_t)(ID_CLS_PACK >> 32);
 constexpr uint32_t CLS_PX_LO = (uint32_t)CLS_PX_PACK, CLS_PX_HI = (uint32_t)(CLS_PX_PACK >> 32);
+#endif
 __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32_t W, const uint32_t* sdl,
-                                                 bool& bad) {
+                                                 const uint2* idt, bool& bad) {
   const uint32_t pfx = ev & 7u;
 #ifndef NICE_PLACE_BRANCHY
   // prefix tests as bits of one mask: as == compares of one value, the
@@ -1195,12 +1198,20 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
   const uint32_t s0 = (ev >> 3) & 511u, s1 = (ev >> 12) & 255u, s2 = (ev >> 20) & 255u, s3 = (ev >> 7) & 31u;
   const uint32_t s0l = s0 & 15u;   // LUMA: the reference (bits 3..6)
   const uint32_t id = min(isbr ? s0 : 5u + s0l, 15u);
+#ifndef NICE_PLACE_ARITH
+  // class and offset + 3 of the reference from the block's 16-entry table
+  // (one 8-byte LDS read instead of two packed-constant extractions, one of
+  // them across a word boundary, which compiled to a branch)
+  const uint2 ct = idt[id];
+  const uint32_t cls = ct.x, off3 = ct.y;
+#else
   const uint32_t cls = (id < 8u ? ID_CLS_LO >> (4u * id) : ID_CLS_HI >> (4u * id - 32u)) & 15u;
   const uint32_t rows = (CLS_ROWS_PACK >> (2u * cls)) & 3u;
   const uint32_t b3 = 3u * cls;   // px + 3 at bits 3cls (48 bits over two words)
   const uint32_t pxp = (b3 < 32u ? (CLS_PX_LO >> b3) | (b3 > 29u ? CLS_PX_HI << (32u - b3) : 0u)
                                  : CLS_PX_HI >> (b3 - 32u)) & 7u;
   const uint32_t off3 = rows * W + pxp;   // offset + 3
+#endif
   const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0l >= 11u) || off3 < 3u || q + 3u < off3;
   const uint32_t gl = (s1 - 32u) & 255u;
   const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
@@ -1224,6 +1235,13 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
 
 __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
   __shared__ uint32_t sdl[343];   // SMALL_DIFF index -> constant (code.rs:230-247)
+  __shared__ uint2 idt[16];       // reference id -> {class, rows * W + px + 3}
+  if (threadIdx.x < 16u) {
+    const uint32_t id = threadIdx.x;
+    const uint32_t cls = (uint32_t)(ID_CLS_PACK >> (4u * id)) & 15u;
+    idt[id] = make_uint2(cls, (uint32_t)((CLS_ROWS_PACK >> (2u * cls)) & 3u) * a.W +
+                                  (uint32_t)((CLS_PX_PACK >> (3u * cls)) & 7u));
+  }
   for (uint32_t i = threadIdx.x; i < 343u; i += blockDim.x) {
     const uint32_t rd = i % 7u, t1 = i / 7u;
     sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
@@ -1298,7 +1316,7 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
           qb[k] = base + incl - c32[k];
           base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
           bool rbad = false;
-          r[k] = place_record(ev[k], min(qb[k], N32), a.W, sdl, rbad);
+          r[k] = place_record(ev[k], min(qb[k], N32), a.W, sdl, idt, rbad);
           stop = stop || (valid && (qb[k] >= N32 || (run ? qb[k] + c32[k] > N32 : rbad)));
         }
         if (!__any(stop)) {
@@ -1335,7 +1353,7 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
       carry += __shfl(incl, 63);
       qk[k] = qb;
       bool rbad = false;
-      r[k] = place_record(ev[k], (uint32_t)min(qb, N), a.W, sdl, rbad);
+      r[k] = place_record(ev[k], (uint32_t)min(qb, N), a.W, sdl, idt, rbad);
       const bool at_n = valid && qb == N;
       const bool bad = valid && !at_n && (run ? qb + c[k] > N : rbad);
       const unsigned long long m = __ballot(at_n || bad);
