@@ -55,7 +55,7 @@ struct EncLayout {
   size_t zero_bytes, total;
   size_t o_hist, o_flags, o_ctr, o_status, o_overn, o_overl;
   size_t o_first, o_last, o_next, o_tbl, o_tblcode, o_len8, o_smax, o_seedbit, o_seedsuf,
-      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc, o_bhist;
+      o_hdrbytes, o_hdrcache, o_hdrbitoff, o_recs, o_tbits, o_toff, o_dend, o_packtab, o_gacc, o_bhist, o_cmask;
 };
 
 EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
@@ -88,6 +88,7 @@ EncLayout enc_layout(uint32_t n_frames, uint32_t T, uint64_t npx) {
   L.o_packtab = take((size_t)n_frames * sizeof(PackTab));
   L.o_gacc = take((size_t)n_frames * ((T + ENC_GROUP_TILES - 1) / ENC_GROUP_TILES + 1) * 8);
   L.o_bhist = take((size_t)N_BINS * 4);   // band API: the band's own histogram
+  L.o_cmask = take((size_t)n_frames * T * (ENC_TILE / 32) * 4);   // 1 bit per pixel
   L.total = o;
   return L;
 }
@@ -250,6 +251,7 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.tile_first = (uint32_t*)(base + L.o_first);
   a.tile_last = (uint32_t*)(base + L.o_last);
   a.tile_next = (uint32_t*)(base + L.o_next);
+  a.cmask = (uint32_t*)(base + L.o_cmask);
   a.tbl = (uint32_t*)(base + L.o_tbl);
   a.tbl_code = (uint32_t*)(base + L.o_tblcode);
   a.tbl_len8 = base + L.o_len8;
@@ -346,7 +348,10 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
       else hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_PAIR:
-      hipLaunchKernelGGL(enc_classify_pair, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      // frames: coded flags out, run digits by enc_rundigits (below); bands:
+      // run digits in the kernel
+      if (a.cmask) hipLaunchKernelGGL(enc_classify_pair_m, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(enc_classify_pair, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_RING2:
       if (rgb) hipLaunchKernelGGL(enc_classify_ring2_3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
@@ -399,6 +404,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
     launch_classify(ctx, ck, a, total_tiles, h, st);
+    if (ck == CLS_K_PAIR)   // the run digits of runs inside tiles, from the coded flags
+      hipLaunchKernelGGL(enc_rundigits, dim3(std::min<uint32_t>((T + 7) / 8, 64u), n_frames), dim3(256), 0, st, a);
     ctx->last_classify = (int)ck;
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
@@ -898,6 +905,7 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->band.ptr;
   EncArgs a = enc_args(L, base, 1, w, h, channels, channels_out, T, N);
+  a.cmask = nullptr;   // band tiles: the pair kernel counts its run digits itself
   // virtual bases: global pixel index g addresses d_px + (g - px0) * channels,
   // band records are stored from the band's first pixel
   a.px = d_px - (int64_t)px0 * channels;

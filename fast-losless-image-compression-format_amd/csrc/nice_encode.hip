@@ -868,7 +868,9 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
 // ring holds 3W + 3 pixels behind the pair plus the pair and the next one:
 // 3W + 3 + 4096 <= RING.
 // ---------------------------------------------------------------------------
-template <int C, int RING>
+// MASK_OUT (frames): the coded flags go out to a.cmask and enc_rundigits counts
+// the run digits from them; false (bands): the digits are counted here.
+template <int C, int RING, bool MASK_OUT = false>
 __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
   constexpr int PQ = 2 * CLS_PPT;   // pixel slots per thread (4)
   __shared__ uint32_t ring[RING + CLS_GUARD];
@@ -1005,6 +1007,11 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
         const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
         mask[wb] = (uint32_t)bal;
         mask[wb + 1] = (uint32_t)(bal >> 32);
+        if constexpr (MASK_OUT) {   // tiles tt, tt + 1 are consecutive: one 64-word range
+          uint32_t* cm = a.cmask + it.tile() * (ENC_TILE / 32);
+          cm[wb] = (uint32_t)bal;
+          cm[wb + 1] = (uint32_t)(bal >> 32);
+        }
       }
       coded_bits |= (coded ? 1u : 0u) << q;
     }
@@ -1064,6 +1071,7 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
       slot_hist_add(hs, rec[q]);
       // a run follows only if the next pixel is uncoded; runs crossing the
       // tile's end are enc_tailruns' (lane 63's next pixel is in the next wave)
+      if constexpr (MASK_OUT) continue;   // enc_rundigits counts them
       const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
       if (coded && !next_coded) {
         const int j = q >> 1, pl = p - j * ENC_TILE;   // tile and index in it
@@ -1098,6 +1106,71 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_3(EncArgs a) {
 // (RGBA; an RGB pair's 6 KB byte stage would push the block past 80 KB of LDS,
 // one block per CU)
 __global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_pair(EncArgs a) { enc_classify_pair_body<4, CLS_RING>(a); }
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_pair_m(EncArgs a) {
+  enc_classify_pair_body<4, CLS_RING, true>(a);
+}
+
+// ---------------------------------------------------------------------------
+// K1r: run digits of the runs inside tiles (code.rs:371-407: a run between two
+// coded pixels of one tile, length L >= 1, adds the base-8 digits of L - 1 to
+// the run prefixes' bins; runs that cross a tile's end are enc_tailruns'),
+// from the coded flags enc_classify_pair_m wrote, one 32-pixel word per lane.
+// Counting them inside the classify loop cost that loop 17 % (21.2 vs 17.5 ms
+// per 512 4K frames without the block), in its branches and live state.  A
+// run ends at each coded pixel whose previous pixel is uncoded; its start is
+// the previous coded pixel of the word, or the last coded pixel of the tile's
+// earlier words (a max scan over the half-wave), or none in the tile (skipped).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_rundigits(EncArgs a) {
+  __shared__ uint32_t bins[8];
+  if (threadIdx.x < 8) bins[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t f = blockIdx.y, T = a.tiles_per_frame;
+  const uint32_t lane = threadIdx.x & 63u, k = lane & 31u;
+  const uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwv = gridDim.x * (blockDim.x >> 6);
+  uint32_t cnt[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  for (uint32_t t0 = 2u * wv; t0 < T; t0 += 2u * nwv) {   // lanes 0-31: tile t0, 32-63: tile t0 + 1
+    const uint32_t t = t0 + (lane >> 5);
+    const uint32_t m = t < T ? a.cmask[((uint64_t)f * T + t) * (ENC_TILE / 32) + k] : 0u;
+    // last coded pixel of the tile before this word (-1: none)
+    int inc = m ? (int)(32u * k + 31u - (uint32_t)__clz((int)m)) : -1;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if ((int)k >= o) inc = max(inc, v);
+    }
+    int before = __shfl_up(inc, 1);
+    uint32_t pm = __shfl_up(m, 1);
+    if (k == 0u) { before = -1; pm = 0x80000000u; }   // (a run into the tile: not counted here)
+    uint32_t tb = m & ~((m << 1) | (pm >> 31));        // coded pixels after an uncoded one
+    while (tb) {
+      const uint32_t b = (uint32_t)__builtin_ctz(tb);
+      tb &= tb - 1u;
+      const uint32_t below = m & ((1u << b) - 1u);
+      const int prev = below ? (int)(32u * k + 31u - (uint32_t)__clz((int)below)) : before;
+      if (prev >= 0) {
+        uint32_t mm = (uint32_t)((int)(32u * k + b) - prev - 2);
+        while (true) {
+          const uint32_t d = mm & 7u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cnt[j] += d == (uint32_t)j ? 1u : 0u;
+          if (mm < 8u) break;
+          mm >>= 3;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {   // wave sums, then one LDS add per wave and bin
+    uint32_t v = cnt[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0 && v) atomicAdd(&bins[j], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && bins[threadIdx.x])
+    atomicAdd(&a.hist[(uint64_t)f * N_BINS + BIN_PREFIX + P_RUN1 + threadIdx.x], bins[threadIdx.x]);
+}
 
 // ---------------------------------------------------------------------------
 // K1s: classify, strip-staged (RGBA frames with W % 1024 == 0 too wide for the

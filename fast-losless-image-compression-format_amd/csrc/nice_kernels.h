@@ -31,6 +31,7 @@ struct EncArgs {
   uint32_t* tile_first;      // n_frames * T
   uint32_t* tile_last;       // n_frames * T
   uint32_t* tile_next;       // n_frames * T
+  uint32_t* cmask;           // n_frames * T * 32: coded-pixel flags per tile (enc_classify_pair_m); null in band mode
   uint32_t* tbl;             // n_frames * 858: (code << 5) | len for len <= 25
   uint32_t* tbl_code;        // n_frames * 858: code as u32 (serial path)
   uint8_t* tbl_len8;         // n_frames * 858: u8 length
@@ -95,6 +96,8 @@ __global__ void enc_classify_ring2_3(EncArgs a);
 constexpr uint32_t CLS_RING2_MAX_W = 10239;
 // enc_classify_pair: RGBA, two tiles per iteration, 16K ring: 3W + 3 + 4096 <= 16384
 __global__ void enc_classify_pair(EncArgs a);
+__global__ void enc_classify_pair_m(EncArgs a);
+__global__ void enc_rundigits(EncArgs a);
 constexpr uint32_t CLS_PAIR_MAX_W = 4095;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
 constexpr uint32_t DEC_PARSE_THREADS = 512;
