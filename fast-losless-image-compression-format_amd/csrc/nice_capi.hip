@@ -343,9 +343,11 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
       hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     }
-    case CLS_K_RING:
-      if (rgb) hipLaunchKernelGGL(enc_classify_ring3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
-      else hipLaunchKernelGGL(enc_classify_ring, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+    case CLS_K_RING:   // (frames: the _m forms, as for the pair kernel below)
+      if (rgb) hipLaunchKernelGGL(a.cmask ? enc_classify_ring3_m : enc_classify_ring3, dim3((uint32_t)blocks),
+                                  dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(a.cmask ? enc_classify_ring_m : enc_classify_ring, dim3((uint32_t)blocks),
+                              dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_PAIR:
       // frames: coded flags out, run digits by enc_rundigits (below); bands:
@@ -354,8 +356,10 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
       else hipLaunchKernelGGL(enc_classify_pair, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_RING2:
-      if (rgb) hipLaunchKernelGGL(enc_classify_ring2_3, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
-      else hipLaunchKernelGGL(enc_classify_ring2, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      if (rgb) hipLaunchKernelGGL(a.cmask ? enc_classify_ring2_3_m : enc_classify_ring2_3, dim3((uint32_t)blocks),
+                                  dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(a.cmask ? enc_classify_ring2_m : enc_classify_ring2, dim3((uint32_t)blocks),
+                              dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     case CLS_K_TINY:
       hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
@@ -404,7 +408,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
     launch_classify(ctx, ck, a, total_tiles, h, st);
-    if (ck == CLS_K_PAIR)   // the run digits of runs inside tiles, from the coded flags
+    if (ck == CLS_K_PAIR || ck == CLS_K_RING || ck == CLS_K_RING2)   // in-tile run digits, from the coded flags
       hipLaunchKernelGGL(enc_rundigits, dim3(std::min<uint32_t>((T + 7) / 8, 64u), n_frames), dim3(256), 0, st, a);
     ctx->last_classify = (int)ck;
     tm.end(st);

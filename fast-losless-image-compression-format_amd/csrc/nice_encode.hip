@@ -650,7 +650,9 @@ __device__ __forceinline__ uint32_t px_word(const uint8_t* fr, int64_t j) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
 }
 
-template <int C, int RING>
+// MASK_OUT: as enc_classify_pair_body's (frames: coded flags out, run digits by
+// enc_rundigits).
+template <int C, int RING, bool MASK_OUT = false>
 __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
   __shared__ uint32_t ring[RING + CLS_GUARD];
   __shared__ uint32_t stage[C == 3 ? RGB_TILE_DW + 4 : 1];
@@ -786,6 +788,11 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
         const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
         mask[wb] = (uint32_t)bal;
         mask[wb + 1] = (uint32_t)(bal >> 32);
+        if constexpr (MASK_OUT) {
+          uint32_t* cm = a.cmask + it.tile() * (ENC_TILE / 32);
+          cm[wb] = (uint32_t)bal;
+          cm[wb + 1] = (uint32_t)(bal >> 32);
+        }
       }
       coded_bits |= (coded ? 1u : 0u) << q;
     }
@@ -830,6 +837,7 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
       slot_hist_add(hs, rec[q]);
       // a run follows only if the next pixel is uncoded: most coded lanes stop
       // at this one bit test (lane 63's next pixel is in the next wave: full path)
+      if constexpr (MASK_OUT) continue;   // enc_rundigits counts them
       const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
       if (coded && !next_coded) {
         // next coded pixel: in this wave's 64 pixels from the ballot, else the tile mask
@@ -1097,11 +1105,23 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
 
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring(EncArgs a) { enc_classify_ring_body<4, CLS_RING>(a); }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3(EncArgs a) { enc_classify_ring_body<3, CLS_RING>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring_m(EncArgs a) {
+  enc_classify_ring_body<4, CLS_RING, true>(a);
+}
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring3_m(EncArgs a) {
+  enc_classify_ring_body<3, CLS_RING, true>(a);
+}
 // a 32K-pixel ring (128 KB, one block per CU) for rows of up to
 // CLS_RING2_MAX_W pixels: RGBA widths the strip kernel does not take (W %
 // 1024 != 0, e.g. 7680 for 8K UHD) and RGB frames
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2(EncArgs a) { enc_classify_ring_body<4, 2 * CLS_RING>(a); }
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_3(EncArgs a) { enc_classify_ring_body<3, 2 * CLS_RING>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_m(EncArgs a) {
+  enc_classify_ring_body<4, 2 * CLS_RING, true>(a);
+}
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_ring2_3_m(EncArgs a) {
+  enc_classify_ring_body<3, 2 * CLS_RING, true>(a);
+}
 // pairs of tiles per iteration (16K ring: W <= CLS_PAIR_MAX_W)
 // (RGBA; an RGB pair's 6 KB byte stage would push the block past 80 KB of LDS,
 // one block per CU)

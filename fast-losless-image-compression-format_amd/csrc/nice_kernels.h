@@ -97,6 +97,10 @@ constexpr uint32_t CLS_RING2_MAX_W = 10239;
 // enc_classify_pair: RGBA, two tiles per iteration, 16K ring: 3W + 3 + 4096 <= 16384
 __global__ void enc_classify_pair(EncArgs a);
 __global__ void enc_classify_pair_m(EncArgs a);
+__global__ void enc_classify_ring_m(EncArgs a);
+__global__ void enc_classify_ring3_m(EncArgs a);
+__global__ void enc_classify_ring2_m(EncArgs a);
+__global__ void enc_classify_ring2_3_m(EncArgs a);
 __global__ void enc_rundigits(EncArgs a);
 constexpr uint32_t CLS_PAIR_MAX_W = 4095;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
