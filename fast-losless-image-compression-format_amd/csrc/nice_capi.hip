@@ -340,7 +340,7 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
     case CLS_K_STRIP: {
       uint32_t sblocks;
       a.tiles_per_block = strip_rows(ctx, a.n_frames, a.W, rows_total, &sblocks);
-      hipLaunchKernelGGL(enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
+      hipLaunchKernelGGL(a.cmask ? enc_classify_strip_m : enc_classify_strip, dim3(sblocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
     }
     case CLS_K_RING:   // (frames: the _m forms, as for the pair kernel below)
@@ -408,8 +408,10 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     PhaseTimer& tm = ctx->timer;
     tm.begin(NICE_PH_ENC_CLASSIFY, st);
     launch_classify(ctx, ck, a, total_tiles, h, st);
-    if (ck == CLS_K_PAIR || ck == CLS_K_RING || ck == CLS_K_RING2)   // in-tile run digits, from the coded flags
-      hipLaunchKernelGGL(enc_rundigits, dim3(std::min<uint32_t>((T + 7) / 8, 64u), n_frames), dim3(256), 0, st, a);
+    if (ck != CLS_K_WINDOW && ck != CLS_K_TINY)   // in-tile run digits, from the coded flags
+      hipLaunchKernelGGL(enc_rundigits,
+                         dim3(std::min<uint32_t>((T + 7) / 8, std::max<uint32_t>(64u, 2048u / n_frames)), n_frames),
+                         dim3(256), 0, st, a);   // (>= 2048 blocks in all for few, large frames)
     ctx->last_classify = (int)ck;
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);

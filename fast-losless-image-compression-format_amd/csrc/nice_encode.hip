@@ -1207,7 +1207,8 @@ constexpr int STRIP_W = 2048;
 constexpr int STRIP_RS = STRIP_W + 8;              // window words (+3 each side, padded)
 constexpr int STRIP_LD = (STRIP_W + 6 + CLS_THREADS - 1) / CLS_THREADS;   // window loads per thread (5)
 
-__global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
+template <bool MASK_OUT>
+__device__ __forceinline__ void enc_classify_strip_body(const EncArgs& a) {
   __shared__ uint32_t win[4][STRIP_RS];
   __shared__ uint32_t hs[C0_N + 2 * SX_N];
   __shared__ uint32_t run_hist[8];
@@ -1296,6 +1297,11 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
           const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
           mask[j][wb] = (uint32_t)bal;
           mask[j][wb + 1] = (uint32_t)(bal >> 32);
+          if constexpr (MASK_OUT) {   // (frames: every tile is the block's)
+            uint32_t* cm = a.cmask + ((uint64_t)f * T + (y * W + x0) / ENC_TILE + j) * (ENC_TILE / 32);
+            cm[wb] = (uint32_t)bal;
+            cm[wb + 1] = (uint32_t)(bal >> 32);
+          }
         }
         coded_bits |= (coded ? 1u : 0u) << (2 * j + q);
       }
@@ -1347,6 +1353,7 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
         const bool coded = (coded_bits >> (2 * j + q)) & 1u;
         recs[p] = rec[q];
         slot_hist_add(hs, rec[q]);
+        if constexpr (MASK_OUT) continue;   // enc_rundigits counts the run digits
         const bool next_coded = lane < 63 && ((wbal[j][q] >> (lane + 1)) & 1ull);
         if (coded && !next_coded) {
           const unsigned long long above = lane < 63 ? (wbal[j][q] >> (lane + 1)) : 0ull;
@@ -1370,6 +1377,9 @@ __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) {
     if (v) atomicAdd(&a.hist[(uint64_t)f * N_BINS + k], v);
   }
 }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) { enc_classify_strip_body<false>(a); }
+// frames: the tiles' coded flags out, run digits by enc_rundigits
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip_m(EncArgs a) { enc_classify_strip_body<true>(a); }
 
 // ---------------------------------------------------------------------------
 // K2: runs crossing tile ends. One block (1024 threads) per frame.

@@ -85,6 +85,7 @@ __global__ void enc_classify(EncArgs a);        // W >= 3
 __global__ void enc_classify_tiny(EncArgs a);   // W < 3
 __global__ void enc_classify_ring(EncArgs a);    // RGBA
 __global__ void enc_classify_ring3(EncArgs a);   // RGB, 4-byte aligned frames
+__global__ void enc_classify_strip_m(EncArgs a);
 __global__ void enc_classify_strip(EncArgs a);   // RGBA, W % 1024 == 0, W > CLS_RING_MAX_W (tiles_per_block = rows per block)
 constexpr uint32_t STRIP_W_HOST = 2048;          // == STRIP_W (nice_encode.hip)
 // the 16K-pixel ring holds 3W + 3 pixels of references plus two tiles (the one
