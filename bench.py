@@ -159,7 +159,7 @@ def load_traffic(phase, frames, path=None):
         with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
-        return None
+        return None, None
     for k in PHASE_KERNELS.get(phase, [phase]):
         if k in d.get("kernels", {}):
             return int(d["kernels"][k]["hbm_bytes_per_frame"] * frames), os.path.basename(path)

@@ -147,8 +147,11 @@ struct BandState {
   bool classified = false, tabled = false;
   nice::EncArgs a{};
   uint64_t band_bits = 0, seed_bit = 0;
+  // the band's own symbol counts (nice_band_runs), for its bit count
   uint32_t* bhist = nullptr;
-  const unsigned long long* d_info = nullptr;   // nice_band_tables_dev's output (checked by the pack)   // the band's own symbol counts (nice_band_runs), for its bit count
+  // nice_band_tables_dev's {band bits, data start}, copied into the context
+  // (band_hdr): the pack compares the caller's band_bits with it
+  const unsigned long long* d_info = nullptr;
 };
 
 struct nice_ctx {
@@ -166,6 +169,9 @@ struct nice_ctx {
   const uint32_t* split_abort = nullptr;
   uint32_t split_frames = 0;
   int last_classify = -1;   // ClsKind of the last encode / band classify (test hook nice_test_last_classify)
+  // test hooks (nice_test_set_hooks; 0 = off): the last strip of every split
+  // decode returns at entry; enc_pack's LDS group buffer in bits per pixel
+  uint32_t test_split_absent = 0, test_pack_cap_bpp = 0;
 };
 
 extern "C" {
@@ -285,10 +291,6 @@ EncArgs enc_args(const EncLayout& L, uint8_t* base, uint32_t n_frames, uint32_t 
   a.over_count = (uint32_t*)(base + L.o_overn);
   a.over_list = (uint2*)(base + L.o_overl);
   a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * NICE_PACK_CAP_BPP;
-  if (const char* ev = getenv("NICE_ENC_PACK_CAP")) {   // tests: bits per pixel of the LDS buffer
-    const int b = atoi(ev);
-    if (b >= 1 && b <= NICE_PACK_CAP_BPP) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * (uint32_t)b;
-  }
   return a;
 }
 }  // namespace
@@ -397,6 +399,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->enc.ptr;
   EncArgs a = enc_args(L, base, n_frames, w, h, channels, channels_out, T, N);
+  if (ctx->test_pack_cap_bpp) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * ctx->test_pack_cap_bpp;
   a.px = d_px;
   a.frame_stride = frame_stride;
   a.out = d_out;
@@ -784,6 +787,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // the last sync iteration (no entry changed) already produced chunk_px
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
+  // strict: the reads where the reference's refill loop would wrap (frames
+  // whose tables are all <= 25 bits return at once)
+  if (flags & NICE_DEC_STRICT_REFERENCE) hipLaunchKernelGGL(dec_strict_refill, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a);
   tm.end(st);
   tm.begin(NICE_PH_DEC_EMIT, st);
   if (a.ev) hipLaunchKernelGGL(dec_heads, dim3(n_frames), dim3(1024), 0, st, a);
@@ -823,7 +829,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     size_t lds = ((size_t)SPLIT_THREADS_HOST * 7 + 4 + 4 * ((size_t)sps * 16 + 6 + ((sps * 16 + 6) >> 4) + 17)) * 4;
     lds = std::max<size_t>(lds, 82 * 1024);
     NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    a.test_absent_strip = getenv("NICE_TEST_SPLIT_ABSENT") ? 1u : 0u;
+    a.test_absent_strip = ctx->test_split_absent;
     for (uint32_t f0 = 0; f0 < n_frames; f0 += split_frames) {
       a.split_f0 = f0;
       hipLaunchKernelGGL(dec_rows_split, dim3(std::min(split_frames, n_frames - f0) * strips),
@@ -911,6 +917,7 @@ int nice_band_classify(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint64_
   if (rc) return rc;
   uint8_t* base = (uint8_t*)ctx->band.ptr;
   EncArgs a = enc_args(L, base, 1, w, h, channels, channels_out, T, N);
+  if (ctx->test_pack_cap_bpp) a.pack_cap_bits = (uint32_t)PACK_SUB * ENC_TILE * ctx->test_pack_cap_bpp;
   a.cmask = nullptr;   // band tiles: the pair kernel counts its run digits itself
   // virtual bases: global pixel index g addresses d_px + (g - px0) * channels,
   // band records are stored from the band's first pixel
@@ -1013,11 +1020,15 @@ int nice_band_tables_dev(nice_ctx* ctx, void* stream, const uint32_t* d_hist_tot
   NICE_HIP(hipSetDevice(ctx->device));
   int rc = ctx->band_hdr.grow(4096 + 64);
   if (rc) return rc;
-  if ((rc = band_tables(ctx, (hipStream_t)stream, d_hist_total, (unsigned long long*)d_info))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = band_tables(ctx, st, d_hist_total, (unsigned long long*)d_info))) return rc;
+  // the context's own copy: the caller's buffer may be freed or reused before the pack
+  unsigned long long* mine = (unsigned long long*)((uint8_t*)ctx->band_hdr.ptr + 4096 + 32);
+  NICE_HIP(hipMemcpyAsync(mine, d_info, 16, hipMemcpyDeviceToDevice, st));
   ctx->bs.tabled = true;
   ctx->bs.band_bits = ~0ull;   // known to the caller once d_info is read (nice_band_pack_bits)
   ctx->bs.seed_bit = ~0ull;
-  ctx->bs.d_info = (const unsigned long long*)d_info;
+  ctx->bs.d_info = mine;
   return NICE_OK;
 }
 
@@ -1030,7 +1041,7 @@ static uint64_t band_data_words(uint64_t band_bit0, uint64_t band_bits) {
 }
 
 uint64_t nice_band_words(uint64_t band_bit0, uint64_t band_bits) {
-  return band_bits ? band_data_words(band_bit0, band_bits) + 2 : 0;
+  return band_data_words(band_bit0, band_bits) + 2;   // every band has its trailer (status, deferred write)
 }
 
 int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_t band_bits, uint32_t* d_words,
@@ -1040,7 +1051,6 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   if (nw > words_cap || (nw && !d_words)) return NICE_E_ARG;
   if (ctx->bs.seed_bit != ~0ull && band_bit0 < ctx->bs.seed_bit) return NICE_E_ARG;
   ctx->bs.band_bits = band_bits;
-  if (nw == 0) return NICE_OK;
   NICE_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   EncArgs a = ctx->bs.a;
@@ -1049,6 +1059,15 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   a.out_stride = 0;
   a.band_fix = d_words + (nw - 2);
   NICE_HIP(hipMemsetAsync(a.band_fix, 0, 8, st));
+  // the bit count the caller read back must be the device's: on a mismatch the
+  // pack kernels skip the band and the trailer carries BAND_FIX_BAD, which
+  // nice_band_assemble reports
+  if (ctx->bs.d_info)
+    hipLaunchKernelGGL(enc_band_check, dim3(1), dim3(64), 0, st, a, ctx->bs.d_info, (unsigned long long)band_bits);
+  if (band_bits == 0) {   // no data words: the trailer only
+    NICE_HIP(hipGetLastError());
+    return NICE_OK;
+  }
   // the first word holds the previous band's last bits: only OR-ed into (enc_edges)
   NICE_HIP(hipMemsetAsync(d_words, 0, 4, st));
   const uint32_t nt = a.tile_hi - a.tile_lo;
@@ -1056,8 +1075,6 @@ int nice_band_pack_bits(nice_ctx* ctx, void* stream, uint64_t band_bit0, uint64_
   NICE_HIP(hipMemsetAsync(a.status, 0, (size_t)ng * 8, st));
   NICE_HIP(hipMemsetAsync(a.pack_ctr, 0, 4, st));
   NICE_HIP(hipMemsetAsync(a.over_count, 0, 4, st));
-  if (ctx->bs.d_info)   // the bit count the caller read back must be the device's
-    hipLaunchKernelGGL(enc_band_check, dim3(1), dim3(64), 0, st, a, ctx->bs.d_info, (unsigned long long)band_bits);
   // FLAG_LONG (the launches return at once otherwise): tile bits, their scan from
   // band_bit0, the codes that fit the cache, then the wrapped writes
   const uint32_t tblocks = std::min<uint32_t>(nt, 2048u);
@@ -1087,8 +1104,9 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
     return NICE_E_ARG;
   // the data start: learned by nice_band_tables, else the first band's start
   const uint64_t seed = ctx->bs.seed_bit != ~0ull ? ctx->bs.seed_bit : band_bit0[0];
-  // meta: band first words [R], band offsets [R + 1], data end, out_len, band first bits [R]
-  std::vector<unsigned long long> meta(3 * n_bands + 3);
+  // meta: band first words [R], band offsets [R + 1], data end, out_len, band first bits [R],
+  // status (a band's trailer marked BAND_FIX_BAD: its pack saw a wrong band_bits)
+  std::vector<unsigned long long> meta(3 * n_bands + 4);
   uint64_t off = 0, end = seed;
   for (uint32_t r = 0; r < n_bands; ++r) {
     if (band_bit0[r] != end) return NICE_E_ARG;   // bands must tile the data bits
@@ -1114,13 +1132,13 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
   const uint64_t hdr_words = (seed + 31) >> 5, end_words = (end + 31) >> 5;
   if (end_words > hdr_words)
     NICE_HIP(hipMemsetAsync(d_out + hdr_words * 4, 0, (end_words - hdr_words) * 4, st));
-  if (off) {
+  {
     uint64_t most = 0;
     for (uint32_t r = 0; r < n_bands; ++r) most = std::max<uint64_t>(most, meta[n_bands + r + 1] - meta[n_bands + r]);
     hipLaunchKernelGGL(enc_band_merge, dim3((uint32_t)((most + 4095) / 4096), n_bands), dim3(256), 0, st,
                        (uint32_t*)d_out, d_words, dmeta, dmeta + n_bands, n_bands);
     hipLaunchKernelGGL(enc_band_fix, dim3(1), dim3(64), 0, st, d_out, d_words, dmeta + 2 * n_bands + 3,
-                       dmeta + n_bands, n_bands);
+                       dmeta + n_bands, n_bands, dmeta + 3 * n_bands + 3);
   }
   EncArgs a = ctx->bs.a;
   a.out = d_out;
@@ -1129,7 +1147,13 @@ int nice_band_assemble(nice_ctx* ctx, void* stream, const uint32_t* d_words, con
   a.data_end = dmeta + 2 * n_bands + 1;
   a.out_len = dmeta + 2 * n_bands + 2;
   hipLaunchKernelGGL(enc_tail, dim3(1), dim3(64), 0, st, a);
+  unsigned long long bad = 0;
+  NICE_HIP(hipMemcpyAsync(&bad, dmeta + 3 * n_bands + 3, 8, hipMemcpyDeviceToHost, st));
   NICE_HIP(hipStreamSynchronize(st));   // `meta` lives on this stack frame
+  if (bad) {   // a band was packed with a band_bits other than its own: its bits are missing
+    *out_len = 0;
+    return NICE_E_ARG;
+  }
   *out_len = B + 5;
   NICE_HIP(hipGetLastError());
   return NICE_OK;
@@ -1206,6 +1230,17 @@ int nice_test_occupy(void* stream, uint32_t blocks, uint32_t short_blocks, uint3
 // The classify kernel the context's last encode (or band classify) used:
 // 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip, 5 pair (two tiles per iteration).
 int nice_test_last_classify(nice_ctx* ctx) { return ctx ? ctx->last_classify : -1; }
+
+// Test hooks of one context (tests only; nothing reads the environment for them):
+// split_absent != 0 makes the last strip of every split decode return at entry
+// (a strip that never became resident); pack_cap_bpp in [1, NICE_PACK_CAP_BPP]
+// lowers enc_pack's LDS group buffer to that many bits per pixel (0: default).
+int nice_test_set_hooks(nice_ctx* ctx, uint32_t split_absent, uint32_t pack_cap_bpp) {
+  if (!ctx || pack_cap_bpp > NICE_PACK_CAP_BPP) return NICE_E_ARG;
+  ctx->test_split_absent = split_absent ? 1u : 0u;
+  ctx->test_pack_cap_bpp = pack_cap_bpp;
+  return NICE_OK;
+}
 
 // Frames of the context's last split decode that went to the fallback launch
 // (synchronises the device).

@@ -175,9 +175,9 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
       const int st = threadIdx.x;
       const uint32_t mx = smax[st];
       if (mx < 1 || vseen[st] != mx || vkraft[st] != (1ull << mx)) atomicOr(&bad, 1);
-      // strict: a max length above 24 lets the reference refill loop wrap its u8
-      // bit offset and spin forever (bitreader.rs:88-97): outside its domain
-      if ((a.flags & NICE_DEC_STRICT_REFERENCE) && mx > 24) atomicOr(&bad, 1);
+      // strict: tables of 26..31 bits can make the reference's refill loop wrap
+      // its u8 bit offset (bitreader.rs:88-97); dec_strict_refill finds the reads
+      // where it does
     }
   }
   __syncthreads();
@@ -855,6 +855,108 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// D3b (strict mode only): the reference's refill wrap (bitreader.rs:85-98).
+// read_24bits_noclear(M) refills while its u8 bit offset exceeds 32 - M,
+// subtracting 8 each time; the offset's residue mod 8 is the read position's
+// (offset = P + 32 - 8 * bytes read), so the loop runs through the value P & 7
+// and, when that is above 32 - M, subtracts 8 from it: the u8 wraps and the
+// loop never ends.  A read therefore hangs the reference iff it refills at all
+// -- P + M > 8 * bytes read so far -- and (P & 7) + M > 32 (only M >= 26).
+// Bytes read are a running maximum of ceil((P_k + M_k) / 8) over the reads
+// (M = the stream's max length, hfe.rs:209), starting at the 770 header bytes.
+// The reads that end the decode: every event while pixels < N, then one more
+// prefix (plus the zero digits of a run that reached N, which the reference's
+// run loop keeps reading, code.rs:665-671).  One lane per slice re-parses the
+// converged slice j - 1 (for its reads' running maximum; slices are >= 1024
+// bits and only the last 31 bits of reads matter) and then checks slice j.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_strict_refill(DecArgs a) {
+  __shared__ LutLds S;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
+  const uint32_t f = blockIdx.x / a.chunk_blocks;
+  const uint32_t jb = blockIdx.x % a.chunk_blocks;
+  if (a.status[f] != 0) return;
+  const DecTables* T = reinterpret_cast<const DecTables*>(a.tables) + f;
+  uint32_t mx = 0;
+#pragma unroll
+  for (int st = 0; st < N_STREAMS; ++st) mx = max(mx, (uint32_t)T->max_aob[st]);
+  if (mx <= 25u) return;   // (P & 7) + M <= 32 for every read
+  const uint64_t len = a.stream_len[f];
+  const uint64_t D = a.data_start[f];
+  const uint32_t nc = n_chunks(len, D, a.chunk_bits);
+  if (jb * DEC_PARSE_THREADS >= nc) return;
+  load_lut(S, T);
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6;
+  if (jb * DEC_PARSE_THREADS + wave * 64u >= nc) return;
+  StreamParams SP;
+  SP.load(S);
+  const uint32_t j = jb * DEC_PARSE_THREADS + threadIdx.x;
+  const uint32_t j0 = j > 0 ? j - 1u : 0u;
+  uint32_t* wring = ring + wave * 64u * RING_STRIDE;
+  const uint32_t* my = wring + (threadIdx.x & 63u) * RING_STRIDE;
+  const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const uint64_t base = (uint64_t)f * a.max_chunks;
+  const unsigned long long N = (unsigned long long)a.W * a.H;
+  const unsigned long long begin = D + (unsigned long long)j * a.chunk_bits;
+  const unsigned long long end = begin + a.chunk_bits;
+  const unsigned long long hard = len * 8 + 64;
+  bool active = j < nc;
+  unsigned long long e = 0, q = 0;
+  if (active) {
+    e = j0 == 0 ? 0ull : a.entry[base + j0];
+    q = a.chunk_start[base + j0];
+  }
+  Lane L;
+  L.pos = D + (e & ((1ull << 40) - 1));
+  L.rp = RING_W;
+  uint32_t dk = (uint32_t)(e >> 44) & 127u;
+  bool closed = q == N;
+  unsigned long long nb8 = D;   // 8 x bytes the reference has read (D = 770 bytes)
+  bool hang = false;
+  for (;;) {
+    if (active && (L.pos >= end || L.pos >= hard || q > N)) active = false;
+    if (!__any(active)) break;
+    if (__any(active && !lane_ok(L))) ring_fill<false>(wring, p, len, al16, L);
+    if (!active) continue;
+    const bool chk = L.pos >= begin;   // an event of slice j (not of slice j - 1)
+    // one read of stream st at L.pos, then the symbol
+    auto rd = [&](uint32_t st) -> uint32_t {
+      const uint32_t gp = SP.g[st], M = gp >> 24;
+      if (L.pos + M > nb8) {
+        hang = hang || (chk && (uint32_t)(L.pos & 7u) + M > 32u);
+        nb8 = (L.pos + M + 7u) & ~7ull;
+      }
+      return dsym_gp(L, my, S, st, gp);
+    };
+    const bool at_n = q == N && (dk == 0 || closed);
+    const uint32_t pfx = rd(PFX_STREAM);
+    if (at_n) {
+      // the extra prefix (code.rs:660); a zero digit continues the run loop
+      if (dk != 0 && pfx == (uint32_t)P_RUN1) (void)pixel_count(pfx, dk);
+      else active = false;
+      continue;
+    }
+    if (pfx < (uint32_t)P_RUN1) {
+      (void)rd(pay_stream(pfx, 0));
+      if (pfx == (uint32_t)P_RGB || pfx == (uint32_t)P_LUMA || pfx == (uint32_t)P_LUMA2) {
+        (void)rd(pay_stream(pfx, 1));
+        (void)rd(pay_stream(pfx, 2));
+        if (pfx == (uint32_t)P_LUMA) (void)rd(S_LUMA_OTHER);
+      }
+      q += 1;
+      dk = 0;
+      closed = false;
+    } else {
+      q += pixel_count(pfx, dk);
+      closed = closed || q == N;
+    }
+  }
+  if (hang) set_status(&a.status[f], NICE_E_UNSUPPORTED);
+}
+
+// ---------------------------------------------------------------------------
 // D4: per-pixel records.  With every chunk's entry state and first pixel index
 // known, each chunk decodes its symbols again and writes one 32-bit record per
 // coded pixel; run pixels keep the REC_RUN fill.  A record says how the pixel
@@ -1094,6 +1196,9 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
       if constexpr (FAST) pfx = pixel_event_fast(L, my, S, SP, s0, s1, s2, s3);
       else pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
       if (at_n) {
+        // a zero digit of the run that reached N: the reference's run loop
+        // (code.rs:665-671) reads it and adds nothing
+        if (dk != 0 && pfx == (uint32_t)P_RUN1) { (void)pixel_count(pfx, dk); continue; }
         // the reference still reads one more prefix (code.rs:660): a run digit
         // there makes it copy past its buffer
         err = err || (strict && pfx >= (uint32_t)P_RUN1);
@@ -1354,7 +1459,9 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
       qk[k] = qb;
       bool rbad = false;
       r[k] = place_record(ev[k], (uint32_t)min(qb, N), a.W, sdl, idt, rbad);
-      const bool at_n = valid && qb == N;
+      // a zero-count run event is a zero digit continuing a run (the first
+      // digit counts >= 1): at N the reference's run loop reads it and goes on
+      const bool at_n = valid && qb == N && !(run && c[k] == 0);
       const bool bad = valid && !at_n && (run ? qb + c[k] > N : rbad);
       const unsigned long long m = __ballot(at_n || bad);
       if (stop_k == 4u && m) {
@@ -2036,7 +2143,11 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) h[(W + k) + ((W + k) >> 4)] = v[k].lo;
       }
-      if (lane == nseg - 1) {     // row y+1's left halo: this row's last three pixels
+      // row y+1's left halo: this row's last three pixels -- from the last
+      // segment and, when it holds fewer than three (W % 16 in {1, 2}), the one
+      // before it (round 5 width sweep: W = 66, a row starting with a W+3
+      // reference read a stale halo word)
+      if (x0 + S + 2u >= W) {
         uint32_t* h = ring + (size_t)((y + 1) & (ROWS_RING - 1)) * RS;
 #pragma unroll
         for (int p = 0; p < S; ++p)

@@ -2514,7 +2514,7 @@ __global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncAr
       if (over || !(nw && sh)) a.tile_bits[t0] = 0u;
       if (tt0 + nsub == T) a.data_end[f] = e0;
     }
-    used_words = over ? 0u : nw + 1;   // an over-cap group writes nothing into the buffer   // an over-cap group writes nothing into the buffer
+    used_words = over ? 0u : nw + 1;   // an over-cap group writes nothing into the buffer
     PROF_MARK(4);
     // the next group: claimed only now, when this block can start it at once
     // (a group claimed earlier would keep the look-backs of the groups after
@@ -2766,7 +2766,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_pack_long(EncArgs a, int phas
         }
       } else if (phase == 1) {
         if (a.band && (pos & ~7ull) < a.band_bit0) {   // window reaches the previous band: deferred
-          a.band_fix[0] = 0x80000000u | ((uint32_t)(pos - a.band_bit0) << 8) | n;
+          a.band_fix[0] = BAND_FIX_WRITE | ((uint32_t)(pos - a.band_bit0) << 8) | n;
           a.band_fix[1] = v;
         } else {
           wrapped_write(out, pos, v, n);
@@ -2835,12 +2835,12 @@ __global__ __launch_bounds__(256) void enc_band_merge(uint32_t* out32, const uin
 // The deferred wrapped writes, band by band (their windows are disjoint; each
 // reads the merged bits of the band before it).  One thread: at most R writes.
 __global__ void enc_band_fix(uint8_t* out, const uint32_t* words, const unsigned long long* band_bit0,
-                             const unsigned long long* band_off, uint32_t R) {
+                             const unsigned long long* band_off, uint32_t R, unsigned long long* bad) {
   if (threadIdx.x != 0) return;
   for (uint32_t r = 0; r < R; ++r) {
-    if (band_off[r + 1] == band_off[r]) continue;   // empty band: no trailer
     const uint32_t f = words[band_off[r + 1] - 2];
-    if (f & 0x80000000u) wrapped_write(out, band_bit0[r] + ((f >> 8) & 0xFFu), words[band_off[r + 1] - 1], f & 0xFFu);
+    if (f & BAND_FIX_BAD) *bad = 1;   // packed with a wrong band_bits (enc_band_check)
+    else if (f & BAND_FIX_WRITE) wrapped_write(out, band_bit0[r] + ((f >> 8) & 0xFFu), words[band_off[r + 1] - 1], f & 0xFFu);
   }
 }
 
@@ -2876,8 +2876,11 @@ __global__ __launch_bounds__(256) void enc_band_edges(EncArgs a, uint32_t* edges
 // be the device count (d_info[0]); on a mismatch the band is flagged FLAG_BAD
 // and the pack kernels write nothing (the flag is recomputed on every call)
 __global__ void enc_band_check(EncArgs a, const unsigned long long* info, unsigned long long band_bits) {
-  if (threadIdx.x == 0 && blockIdx.x == 0)
-    a.frame_flags[0] = (a.frame_flags[0] & ~FLAG_BAD) | (info[0] != band_bits ? FLAG_BAD : 0u);
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const bool bad = info[0] != band_bits;
+    a.frame_flags[0] = (a.frame_flags[0] & ~FLAG_BAD) | (bad ? FLAG_BAD : 0u);
+    if (bad) a.band_fix[0] = BAND_FIX_BAD;   // reported by nice_band_assemble
+  }
 }
 
 __global__ __launch_bounds__(256) void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info) {

@@ -72,8 +72,8 @@ struct EncArgs {
   uint32_t groups;
   unsigned long long* gacc;
   // enc_pack: bits a group may hold in its LDS buffer (PACK_SUB * ENC_TILE * 32;
-  // NICE_ENC_PACK_CAP=b lowers it to b bits per pixel, so tests reach the
-  // over-cap path on ordinary frames)
+  // the test hook nice_test_set_hooks lowers it to b bits per pixel, so tests
+  // reach the over-cap path on ordinary frames)
   uint32_t pack_cap_bits;
   // groups over that buffer, for enc_pack_over: {frame * groups + group, bits}
   uint32_t* over_count;      // zeroed per launch
@@ -132,8 +132,12 @@ __global__ void enc_tail(EncArgs a);
 __global__ void enc_band_edges(EncArgs a, uint32_t* edges);
 __global__ void enc_band_sum(EncArgs a, const uint32_t* bhist, unsigned long long* info);
 __global__ void enc_band_check(EncArgs a, const unsigned long long* info, unsigned long long band_bits);
+// band trailer word 0: a deferred wrapped write {BAND_FIX_WRITE | offset << 8 |
+// length} (code in word 1), or BAND_FIX_BAD: the band was packed with a
+// band_bits other than its own (nothing written)
+constexpr uint32_t BAND_FIX_WRITE = 0x80000000u, BAND_FIX_BAD = 0x40000000u;
 __global__ void enc_band_fix(uint8_t* out, const uint32_t* words, const unsigned long long* band_bit0,
-                             const unsigned long long* band_off, uint32_t R);
+                             const unsigned long long* band_off, uint32_t R, unsigned long long* bad);
 __global__ void enc_band_merge(uint32_t* out32, const uint32_t* words, const unsigned long long* band_w0,
                                const unsigned long long* band_off, uint32_t R);
 // long-code frames (FLAG_LONG): phase 0 packs every code whose write does not
@@ -201,7 +205,7 @@ struct DecArgs {
   // only frames whose strips could not all be resident (hand_abort ==
   // SPLIT_REDO: a wait timed out) are reconstructed, the others return at once
   uint32_t redo;
-  // tests (NICE_TEST_SPLIT_ABSENT): the last strip of every frame returns at
+  // tests (nice_test_set_hooks): the last strip of every frame returns at
   // once, as a block that never became resident would, so the others time out
   uint32_t test_absent_strip;
 };
@@ -215,6 +219,7 @@ __global__ void dec_tables(DecArgs a);
 __global__ void dec_init_entries(DecArgs a);
 __global__ void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev);
 __global__ void dec_scan(DecArgs a);
+__global__ void dec_strict_refill(DecArgs a);   // NICE_DEC_STRICT_REFERENCE only
 __global__ void dec_emit(DecArgs a);
 __global__ void dec_place(DecArgs a);
 __global__ void dec_heads(DecArgs a);

@@ -121,7 +121,7 @@ class HipBands:
         h = hist_total.to(device=self._dev(), dtype=torch.int32).contiguous()
         info = torch.empty(2, dtype=torch.int64, device=self._dev())
         self._h = h
-        self._info = info   # read again by nice_band_pack_bits (band_bits check)
+        self._info = info   # alive until the call has copied it (stream order)
         self._check(self.L.nice_band_tables_dev(self.ctx.ptr, self._st(), ctypes.c_void_p(h.data_ptr()),
                                                 ctypes.c_void_p(info.data_ptr())), "nice_band_tables_dev")
         return info

@@ -119,19 +119,23 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
  *   5. gather words         nice_band_assemble (one rank): header + bands + tail
  * The result equals nice_encode of the whole image byte for byte, codes longer
  * than 25 bits included.  nice_band_words() counts the band's stream words plus
- * a two-word trailer: a code longer than 25 bits that starts in the byte
- * holding band_bit0 rewrites (reference writer wrap, bitwriter.rs:55-73) bits
- * of the previous band; it is recorded there and applied by nice_band_assemble.
+ * a two-word trailer (every band has one, a band of 0 bits only the trailer):
+ * a code longer than 25 bits that starts in the byte holding band_bit0
+ * rewrites (reference writer wrap, bitwriter.rs:55-73) bits of the previous
+ * band; it is recorded there and applied by nice_band_assemble.
  * Device-resident variants (no host synchronisation between the steps; the
  * exchanges can stay on device, e.g. RCCL collectives on the same stream):
  *   nice_band_runs_dev      band_next read from device memory (u32)
  *   nice_band_tables_dev    d_info[0] = the band's data bits, d_info[1] = the
- *                           data start bit (device u64 x 2, written in stream order)
+ *                           data start bit (device u64 x 2, written in stream
+ *                           order; the context keeps its own copy, so d_info may
+ *                           be freed or reused once the call's work has run)
  *   nice_band_pack_bits     the band's bits passed in (from the gathered d_info);
  *                           band_bits must equal d_info[0] exactly (it sizes the
  *                           band's words): after nice_band_tables_dev the device
  *                           compares them and, on a mismatch, writes no band bits
- *                           (d_words is then undefined, never overrun)
+ *                           (d_words never overrun) and marks the band's trailer;
+ *                           nice_band_assemble then returns NICE_E_ARG
  * nice_band_assemble after nice_band_tables_dev takes band_bit0[0] as the data
  * start.
  * d_px holds pixels [px0, px0 + px_count) (global raster index), which must

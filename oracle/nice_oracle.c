@@ -525,8 +525,16 @@ int nice_oracle_encode_bitpos(const uint8_t *in, size_t in_len, uint32_t width, 
 /* stride everywhere (the evident intent), used only to check RGBA round trips.*/
 /* ------------------------------------------------------------------------- */
 typedef struct { uint16_t symbol; uint8_t aob; } lut_t;
+#ifndef LUT_LAZY_BITS
+#define LUT_LAZY_BITS 20
+#endif
 typedef struct {
     uint8_t max_aob; lut_t *lut; size_t lut_len;
+    /* tables over LUT_LAZY_BITS: the 2^max LUT (hfe.rs:191-202) as its code
+     * intervals, lower bounds descending (the domain check makes the code
+     * complete and non-overlapping, so every window value falls in exactly
+     * the interval whose LUT range holds it: same symbol and length) */
+    int nlazy; uint64_t *zlo; uint16_t *zsym; uint8_t *zlen;
     /* tolerant tables (canonical order, decodable entries only) */
     int ncanon; uint32_t *clo; uint16_t *csym; uint8_t *clen;
 } sslookup_t;
@@ -558,6 +566,23 @@ static int read_header_into_tree(bitreader_t *r, sslookup_t *sl, int n) {
     }
     nice_oracle_canonical(a, n, code);
     sl->lut_len = (size_t)1 << (mx & 63u);
+    if (mx > LUT_LAZY_BITS) {
+        sl->zlo = (uint64_t *)malloc(8 * (size_t)n);
+        sl->zsym = (uint16_t *)malloc(2 * (size_t)n);
+        sl->zlen = (uint8_t *)malloc((size_t)n);
+        sl->nlazy = 0;
+        for (int i = 0; i < n; ++i) {             /* insertion by lower bound, descending */
+            uint64_t lo = code[i] << ((uint8_t)(mx - a[i]) & 63u);
+            int k = sl->nlazy++;
+            while (k > 0 && sl->zlo[k - 1] < lo) {
+                sl->zlo[k] = sl->zlo[k - 1]; sl->zsym[k] = sl->zsym[k - 1]; sl->zlen[k] = sl->zlen[k - 1];
+                --k;
+            }
+            sl->zlo[k] = lo; sl->zsym[k] = (uint16_t)i; sl->zlen[k] = a[i];
+        }
+        free(a); free(code);
+        return 0;
+    }
     sl->lut = (lut_t *)calloc(sl->lut_len, sizeof(lut_t));
     int rc = 0;
     for (int i = 0; i < n && !rc; ++i) {
@@ -702,7 +727,17 @@ static inline int read_next_symbol_x(symreader_t *sr, const sslookup_t *sl, unsi
         if (sr->r.hung) return NICE_ORACLE_E_HANG;
     }
     if (v >= sl->lut_len) return NICE_ORACLE_E_PANIC;
-    lut_t l = sl->lut[v];
+    lut_t l;
+    if (sl->zlo) {                                       /* lazy LUT: first lower bound <= v */
+        int lo = 0, hi = sl->nlazy - 1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (sl->zlo[mid] <= v) hi = mid; else lo = mid + 1;
+        }
+        l.symbol = sl->zsym[lo]; l.aob = sl->zlen[lo];
+    } else {
+        l = sl->lut[v];
+    }
     if (sr->intent) sr->bitpos += l.aob;
     else sr->r.bit_offset = (uint8_t)(sr->r.bit_offset + l.aob);
     *sym = l.symbol;
@@ -871,7 +906,10 @@ int nice_oracle_decode(const uint8_t *s, size_t len, int mode, uint8_t **out, si
     }
     (void)v;
 done:
-    for (int k = 0; k < N_STREAMS; ++k) { free(L[k].lut); free(L[k].clo); free(L[k].csym); free(L[k].clen); }
+    for (int k = 0; k < N_STREAMS; ++k) {
+        free(L[k].lut); free(L[k].clo); free(L[k].csym); free(L[k].clen);
+        free(L[k].zlo); free(L[k].zsym); free(L[k].zlen);
+    }
     if (rc) { free(o); return rc; }
     *out = o;
     *out_len = image_size;

@@ -40,3 +40,11 @@ def band_encode(nice, t, w, h, c, R):
     """One image through the band C ABI in one process (sharded.encode_bands)."""
     S = importlib.import_module(PKG_NAME + ".sharded")
     return S.encode_bands(t, w, h, c, R)
+
+
+def set_hooks(nice, ctx, split_absent=0, pack_cap_bpp=0):
+    """The library's per-context test hooks (nice_test_set_hooks)."""
+    import ctypes
+    L = nice.lib()
+    L.nice_test_set_hooks.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    assert L.nice_test_set_hooks(ctx.ptr, split_absent, pack_cap_bpp) == 0

@@ -133,13 +133,7 @@ def test_decode_strict_reference(nice, O, case):
         ok = True
     except nice.NiceError:
         ok = False
-    _, st = O.encode(px, w, h, c, with_stats=True)
-    if ref_ok and max(st.max_aob) > 24:
-        # the one deliberate conservative refusal: a table longer than 24 bits
-        # (the reference's u8 bit offset may wrap on it, bitreader.rs:88-97)
-        assert not ok, name
-    else:
-        assert ok == ref_ok, (name, ok, ref_ok)
+    assert ok == ref_ok, (name, ok, ref_ok)
     if ok:
         assert np.array_equal(np.frombuffer(got, np.uint8), ref)
 
@@ -299,23 +293,30 @@ def test_decode_single_wave_rows(nice, O, monkeypatch):
 
 
 # SYN-v1 RGB frames inside the literal reference decoder's domain (the oracle's
-# reference-mode decode terminates); (256, 64, 8) has a 25-bit table, which
-# strict mode refuses on purpose although the reference decodes it.
+# reference-mode decode terminates; (256, 64, 8) and (200, 64, 4) have 25-bit
+# tables, which never wrap the reference's refill loop), and frames with 26-31
+# bit tables on which the reference's refill loop wraps and never ends
+# (bitreader.rs:85-98): strict mode must fail on exactly those.
 STRICT_DOMAIN = [(512, 512, 1), (512, 512, 2), (333, 211, 3), (640, 480, 4), (1920, 1080, 5),
-                 (1000, 997, 6), (300, 300, 7), (256, 64, 8), (1024, 768, 9), (200, 150, 10)]
+                 (1000, 997, 6), (300, 300, 7), (256, 64, 8), (1024, 768, 9), (200, 150, 10),
+                 (200, 64, 4), (256, 64, 1), (160, 60, 2), (100, 100, 4), (240, 48, 9), (140, 70, 10)]
 
 
 @pytest.mark.parametrize("case", STRICT_DOMAIN, ids=[f"{w}x{h}s{s}" for w, h, s in STRICT_DOMAIN])
 def test_decode_strict_reference_domain(nice, O, case):
-    """Strict mode must decode every stream the literal reference decodes
-    (identical pixels), except the documented refusal of tables over 24 bits."""
+    """Strict mode decodes exactly the streams the literal reference decodes
+    (identical pixels) and refuses the others."""
     w, h, seed = case
     px = O.gen_syn_v1(w, h, 3, seed)
-    s, st = O.encode(px, w, h, 3, with_stats=True)
-    ref, _ = O.decode(s)
-    if max(st.max_aob) > 24:
+    s = O.encode(px, w, h, 3)
+    try:
+        ref, _ = O.decode(s)
+    except O.OracleDecodeError:
         with pytest.raises(nice.NiceError):
             nice.decode_bytes(s, flags=nice.DEC_STRICT_REFERENCE)
+        # the intent decoder reads them correctly
+        got, _ = nice.decode_bytes(s)
+        assert np.array_equal(np.frombuffer(got, np.uint8), px)
         return
     got, _ = nice.decode_bytes(s, flags=nice.DEC_STRICT_REFERENCE)
     assert np.array_equal(np.frombuffer(got, np.uint8), ref)

@@ -4,7 +4,7 @@ A packer group (4 tiles, 4096 pixels) collects its codes in an LDS buffer of
 32 bits per pixel.  A group that goes over it -- only possible after its first
 tiles have already been OR-ed into the buffer -- is counted and OR-ed into the
 output directly instead, and the next group on the block must clear the whole
-buffer.  NICE_ENC_PACK_CAP=b lowers the buffer to b bits per pixel so ordinary
+buffer.  The test hook pack_cap_bpp=b lowers the buffer to b bits per pixel so ordinary
 frames reach that path (mid-group, after tiles were written); a frame with one
 row of noise in a smooth image reaches it at the real cap.  Every stream must
 equal the oracle's byte for byte.
@@ -15,9 +15,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture
+def cap_hook(nice):
+    """Sets the default context's packer cap (bits per pixel); reset after."""
+    from conftest import set_hooks
+    ctx = nice._ctx(0)
+    yield lambda b: set_hooks(nice, ctx, pack_cap_bpp=b)
+    set_hooks(nice, ctx)
+
+
 @pytest.mark.parametrize("cap", [4, 8, 12])
-def test_pack_cap_single_frames(nice, O, cap, monkeypatch):
-    monkeypatch.setenv("NICE_ENC_PACK_CAP", str(cap))
+def test_pack_cap_single_frames(nice, O, cap, cap_hook):
+    cap_hook(cap)
     for w, h, c, seed in [(1920, 1080, 4, 3), (4096, 64, 4, 5), (1000, 333, 3, 2)]:
         px = O.gen_syn_v1(w, h, c, seed)
         want = O.encode(px, w, h, c)
@@ -25,11 +34,11 @@ def test_pack_cap_single_frames(nice, O, cap, monkeypatch):
         assert got == want, (w, h, c, cap)
 
 
-def test_pack_cap_batch(nice, O, monkeypatch):
+def test_pack_cap_batch(nice, O, cap_hook):
     """A batch: blocks move between frames and reuse their LDS buffer across
     over-cap and ordinary groups."""
     import torch
-    monkeypatch.setenv("NICE_ENC_PACK_CAP", "11")   # SYN-v1 averages ~10.7 bits/px: both kinds of group
+    cap_hook(11)   # SYN-v1 averages ~10.7 bits/px: both kinds of group
     w, h, c, n = 1280, 720, 4, 6
     frames = np.stack([O.gen_syn_v1(w, h, c, s) for s in range(1, n + 1)])
     px = torch.from_numpy(frames).cuda()
@@ -45,14 +54,21 @@ def test_pack_cap_batch(nice, O, monkeypatch):
         assert bytes(host[i, :L[i]]) == want, i
 
 
-def test_pack_cap_bands(nice, O, monkeypatch):
+def test_pack_cap_bands(nice, O):
+    import importlib
     import torch
-    from conftest import band_encode
-    monkeypatch.setenv("NICE_ENC_PACK_CAP", "8")
-    w, h, c = 2048, 512, 4
+    from conftest import PKG_NAME, set_hooks
+    S = importlib.import_module(PKG_NAME + ".sharded")
+    w, h, c, R = 2048, 512, 4, 3
     px = O.gen_syn_v1(w, h, c, 4)
     want = O.encode(px, w, h, c)
-    got = band_encode(nice, torch.from_numpy(px).cuda(), w, h, c, 3).cpu().numpy().tobytes()
+    backends = []
+    for _ in range(R):
+        be = S.HipBands(0)
+        be.ctx = nice._Ctx(0)
+        set_hooks(nice, be.ctx, pack_cap_bpp=8)
+        backends.append(be)
+    got = S.encode_bands(torch.from_numpy(px).cuda(), w, h, c, R, backends=backends).cpu().numpy().tobytes()
     assert got == want
 
 

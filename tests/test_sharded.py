@@ -92,6 +92,59 @@ def test_band_api_host_steps(nice, O, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("delta", [+1, -1, "zero"])
+def test_band_pack_wrong_bits_reported(nice, O, delta):
+    """nice_band_pack_bits with a band_bits other than the band's own (after
+    nice_band_tables_dev): nothing is written past the caller's words, and
+    nice_band_assemble returns NICE_E_ARG instead of a corrupt stream.  The
+    d_info tensor is freed and overwritten before the pack (the context keeps
+    its own copy)."""
+    import torch
+    S = _sharded()
+    w, h, c, R = 1000, 700, 4, 3
+    px = torch.from_numpy(O.gen_syn_v1(w, h, c, 7)).cuda()
+    bes = [S.HipBands(0) for _ in range(R)]
+    for be in bes:
+        be.ctx = nice._Ctx(0)
+    ranges = [S.band_tiles(w, h, r, R) for r in range(R)]
+    edges = []
+    for be, (lo, hi) in zip(bes, ranges):
+        p0, p1 = S.band_pixels(w, h, lo, hi)
+        edges.append(be.classify(px[p0 * c: p1 * c], p0, w, h, c, c, lo, hi))
+    nxt = S.band_next_of(torch.stack(edges)[:, 0], w * h).to(torch.int32)
+    hist = torch.stack([be.runs(nxt[r]) for r, be in enumerate(bes)]).sum(0, dtype=torch.int32)
+    infos = [be.tables(hist) for be in bes]
+    info = torch.stack(infos).cpu()
+    for be in bes:   # the caller's d_info buffers go away (the caching allocator reuses them)
+        be._info.fill_(-1)
+        be._info = None
+    del infos
+    torch.cuda.synchronize()
+    bits = [int(x) for x in info[:, 0]]
+    seed = int(info[0, 1])
+    bit0s = [seed + sum(bits[:r]) for r in range(R)]
+    wrong = list(bits)
+    wrong[1] = 0 if delta == "zero" else bits[1] + delta
+    wbit0s = [seed + sum(wrong[:r]) for r in range(R)]   # consistent offsets: only the device sees it
+    parts = []
+    for r, be in enumerate(bes):
+        n = be.words(wbit0s[r], wrong[r])
+        buf = torch.full((n + 64,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        be.pack(wbit0s[r], wrong[r], buf[:n])
+        torch.cuda.synchronize()
+        assert (buf[n:] == 0x5A5A5A5A).all(), r   # the guard words untouched
+        parts.append(buf[:n])
+    with pytest.raises(nice.NiceError):
+        bes[0].assemble(torch.cat(parts), wbit0s, wrong, w, h)
+    # the right counts still assemble the oracle's stream
+    parts = []
+    for r, be in enumerate(bes):
+        parts.append(be.pack(bit0s[r], bits[r]))
+    got = bes[0].assemble(torch.cat(parts), bit0s, bits, w, h).cpu().numpy().tobytes()
+    assert got == O.encode(px.cpu().numpy(), w, h, c)
+
+
+@pytest.mark.gpu
 def test_encode_sharded_world1_rccl(nice, O, tmp_path):
     """encode_sharded over a real process group (nccl = RCCL), one rank."""
     script = tmp_path / "one.py"
@@ -148,7 +201,7 @@ MOCK_WORKER = textwrap.dedent("""
             self.hist_total = int(hist.sum())
             return torch.tensor([1000 * (self.r + 1) + self.r, 6160], dtype=torch.int64)
         def words(self, bit0, bits):
-            return ((bit0 + bits + 31) >> 5) - (bit0 >> 5) + 2 if bits else 0
+            return ((bit0 + bits + 31) >> 5) - (bit0 >> 5) + 2 if bits else 2
         def pack(self, bit0, bits):
             self._fail("pack")
             n = self.words(bit0, bits)
@@ -265,7 +318,7 @@ ORACLE_WORKER = textwrap.dedent("""
             bits = end - start if start is not None else 0
             return torch.tensor([bits, int(self.bit[0])], dtype=torch.int64)
         def words(self, bit0, bits):
-            return ((bit0 + bits + 31) >> 5) - (bit0 >> 5) + 2 if bits else 0
+            return ((bit0 + bits + 31) >> 5) - (bit0 >> 5) + 2 if bits else 2
         def pack(self, bit0, bits):
             n = self.words(bit0, bits)
             if not n:

@@ -201,15 +201,16 @@ def test_split_not_coresident_falls_back(nice, O):
 
 @pytest.mark.parametrize("shape", [(16384, 64, 4), (20000, 24, 3)], ids=["16384x64x4", "20000x24x3"])
 def test_split_absent_strip_redone(nice, O, shape, monkeypatch):
-    """A strip that never becomes resident (NICE_TEST_SPLIT_ABSENT: the last
+    """A strip that never becomes resident (test hook split_absent: the last
     strip of each frame returns at entry): its neighbour's halo wait times out
     (0.2 s), the frame's strips stop, and the fallback launch (dec_rows_wide;
     dec_reconstruct above 16384 columns) reconstructs the frame exactly."""
     import torch
-    monkeypatch.setenv("NICE_TEST_SPLIT_ABSENT", "1")
+    from conftest import set_hooks
     w, h, c = shape
     px = O.gen_syn_v1(w, h, c, 23)
     ctx = nice.Context(0)
+    set_hooks(nice, ctx, split_absent=1)
     t0 = time.time()
     dec, status = _decode_dev(nice, O, px, w, h, c, ctx)
     torch.cuda.synchronize()

@@ -1,0 +1,73 @@
+"""Width sweep: encode bytes and decode pixels against the oracle at every width
+class the kernels treat differently.
+
+Offsets wrap linearly across rows (code.rs:141-145: W-1, W-3, 3W-3, ...), the
+encoder's tiles are 1024 pixels, its ring kernels hold 3W+3 pixels plus one or
+two tiles (routes switch at 4095 / 4777 / 10239), and the decoder's row
+segments are 16 (or 8) pixels with the last segment ragged, its row kernels
+switch at 4096 columns.  Widths near each of those edges, every W % 16 residue
+and every small width 3..80, RGB and RGBA, 12 rows: the stream must equal the
+oracle's byte for byte, and the decode must give back the frame (both segment
+sizes), wherever the oracle's intent decode does (W = 3 streams can make a
+pixel reference itself through offset W - 3 = 0: undecodable by any decoder).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+H = 12
+WIDTHS = {
+    "small": list(range(3, 81)),
+    "res16": list(range(1600, 1616)),
+    "tile1k": list(range(1022, 1027)),
+    "tile2k": list(range(2046, 2051)),
+    "pair4k": list(range(4094, 4099)),
+    "ring": list(range(4775, 4780)),
+    "ring2": list(range(10238, 10242)),
+}
+
+
+def _frame(O, W, C, seed):
+    """SYN-v1 with, on every row, a pixel at column W-3 that only luma
+    reference 3 (offset W-3: pixel 0 of the same row) predicts."""
+    rng = np.random.default_rng(seed)
+    px = O.gen_syn_v1(W, H, C, seed).reshape(H, W, C).copy()
+    if W >= 6:
+        for y in range(H):
+            c = rng.integers(0, 256, 3)
+            px[y, 0, :3] = c
+            px[y, 1, :3] = (c + [1, 2, 3]) % 256
+            px[y, W - 3, :3] = (c + [5, 7, 3]) % 256
+    return px.reshape(-1)
+
+
+def _same(got, want, what):
+    if got != want:
+        d = next((i for i in range(min(len(got), len(want))) if got[i] != want[i]), min(len(got), len(want)))
+        pytest.fail(f"{what}: lengths {len(got)} / {len(want)}, first differing byte {d}")
+
+
+@pytest.mark.parametrize("group", list(WIDTHS))
+def test_width_sweep(nice, O, group, monkeypatch):
+    monkeypatch.setenv("NICE_DEC_SEG", "16")
+    for W in WIDTHS[group]:
+        for C in (3, 4):
+            px = _frame(O, W, C, W * 7 + C)
+            want = O.encode(px, W, H, C)
+            _same(bytes(nice.encode_bytes(px, W, H, C)), want, f"encode W={W} C={C}")
+            rgb = px.reshape(-1, C)[:, :3].reshape(-1)
+            try:
+                ref, _ = O.decode(want[:12] + bytes([3]) + want[13:], O.DEC_TOLERANT)
+                decodable = np.array_equal(ref, rgb)
+            except O.OracleDecodeError:
+                decodable = False
+            if not decodable:
+                assert W == 3, (W, C)
+                continue
+            for seg in ("16", "8"):
+                monkeypatch.setenv("NICE_DEC_SEG", seg)
+                got, img = nice.decode_bytes(want, flags=nice.DEC_TOLERANT_HEADER | nice.DEC_ALPHA_FILL_FF)
+                g = np.frombuffer(got, np.uint8).reshape(-1, C)
+                assert np.array_equal(g[:, :3].reshape(-1), rgb), (W, C, seg)
+            monkeypatch.setenv("NICE_DEC_SEG", "16")

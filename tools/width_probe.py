@@ -1,0 +1,34 @@
+"""Width sweep probe: for each width, which decode paths reproduce the frame
+(first differing pixel otherwise).  Usage: python tools/width_probe.py W0 W1 [H]"""
+import importlib, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
+from oracle import oracle as O
+from test_width_sweep import _frame, H as H0
+nice = importlib.import_module("fast-losless-image-compression-format_amd")
+w0, w1 = int(sys.argv[1]), int(sys.argv[2])
+H = int(sys.argv[3]) if len(sys.argv) > 3 else H0
+import test_width_sweep as T
+T.H = H
+for W in range(w0, w1):
+    for C in (3, 4):
+        px = _frame(O, W, C, W * 7 + C)
+        s = O.encode(px, W, H, C)
+        rgb = px.reshape(-1, C)[:, :3]
+        res = []
+        for name, env in [("seg16", {"NICE_DEC_SEG": "16"}), ("seg8", {"NICE_DEC_SEG": "8"}),
+                          ("single", {"NICE_DEC_SINGLE_WAVE": "1"}), ("slow", {"NICE_DEC_SLOW_PARSE": "1"})]:
+            for k in ("NICE_DEC_SEG", "NICE_DEC_SINGLE_WAVE", "NICE_DEC_SLOW_PARSE"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            try:
+                got, _ = nice.decode_bytes(s, flags=nice.DEC_TOLERANT_HEADER | nice.DEC_ALPHA_FILL_FF)
+                g = np.frombuffer(got, np.uint8).reshape(-1, C)[:, :3]
+                bad = np.nonzero((g != rgb).any(1))[0]
+                res.append(f"{name}:" + ("ok" if len(bad) == 0 else f"{len(bad)}@({bad[0] % W},{bad[0] // W})"))
+            except nice.NiceError as e:
+                res.append(f"{name}:err{e.code}")
+        if any("ok" not in r for r in res):
+            print(W, C, " ".join(res), flush=True)
+print("done")
