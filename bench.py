@@ -374,19 +374,36 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     for i in range(k):
         assert torch.equal(dec[i].view(N, 4)[:, :3], src[i].view(N, 4)[:, :3]), "streamed round trip"
     barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
+    # every timed stream and decoded frame gets a device checksum (nice_pipe_
+    # set_checksums, inside the timed run: part of what is measured), checked
+    # below against the oracle's stream and the source pixels
+    p.checksums(True)
     barrier()
     t0 = time.perf_counter()
     lens = p.encode(frames, o_list)
     t_enc = time.perf_counter() - t0
+    enc_sums = p.last_sums
     barrier()
     t1 = time.perf_counter()
     st = p.decode(o_list, lens, d_list)
     t_dec = time.perf_counter() - t1
+    dec_sums = p.last_sums
     assert st == [0] * n
     # the timed frames, checked outside the timed regions: every frame's stream
-    # length equals its distinct source's (all n encodes, not only the warm-up),
-    # and each decode buffer -- last written by the timed run -- holds its source
-    assert all(lens[i] == lens[i % k] for i in range(n)), "streamed: timed stream lengths differ"
+    # checksum equals that of the oracle's stream of its source (all n
+    # encodes), every decoded frame's equals its source's, and each decode
+    # buffer -- last written by the timed run -- holds its source
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    with ThreadPoolExecutor(min(k, 16)) as ex:   # ctypes calls release the GIL
+        want = list(ex.map(lambda j: O.encode(src[j].numpy(), W, H, 4), range(k)))
+    want_enc = [nice.checksum64(w) for w in want]
+    want_dec = [nice.checksum64(src[j].numpy()) for j in range(k)]
+    assert all(lens[i] == len(want[i % k]) for i in range(n)), "streamed: timed stream lengths differ from the oracle's"
+    bad = [i for i in range(n) if enc_sums[i] != want_enc[i % k]]
+    assert not bad, f"streamed: timed streams {bad[:8]} differ from the oracle's (checksum)"
+    bad = [i for i in range(n) if dec_sums[i] != want_dec[i % k]]
+    assert not bad, f"streamed: timed decodes {bad[:8]} differ from their sources (checksum)"
     for i in range(k):
         assert torch.equal(dec[i].view(N, 4)[:, :3], src[i].view(N, 4)[:, :3]), "streamed timed round trip"
     t_enc = max_over_ranks(t_enc, dist, device)
@@ -399,8 +416,9 @@ def streamed(torch, nice, dist, device, px, W, H, rank, world, total, distinct=1
     return {"workload": f"{n * world} x {W}x{H} RGBA frames from pinned host memory, {n} per GPU, "
                         f"H2D/compute/D2H overlapped ({depth} slots x {batch} frames)",
             "host_numa_node": node,
-            "check": f"all {n} timed streams' lengths equal their source's; the {k} decode buffers after the "
-                     f"timed run equal their sources",
+            "check": f"{n} timed streams checksum-equal (device checksum64, nice.h) to the oracle's stream of "
+                     f"their source ({k} distinct); {n} timed decodes checksum-equal to their source pixels; the "
+                     f"{k} decode buffers after the timed run byte-equal their sources",
             "encode_mpix_s": round(px_all / t_enc / 1e6, 2),
             "decode_mpix_s": round(px_all / t_dec / 1e6, 2),
             "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),

@@ -45,12 +45,12 @@ DEC_TOLERANT_HEADER = 0x4   # repair spilled 5-bit max fields (small / flat imag
 EXPORTS = [
     "nice_version", "nice_device_count", "nice_encode_bound", "nice_encode", "nice_peek_header",
     "nice_decode", "nice_ctx_create", "nice_ctx_destroy", "nice_ctx_reserve",
-    "nice_encode_batch_dev", "nice_decode_batch_dev",
+    "nice_encode_batch_dev", "nice_decode_batch_dev", "nice_decode_batch_dev_hl",
     "nice_band_classify", "nice_band_runs", "nice_band_tables", "nice_band_words", "nice_band_pack",
     "nice_band_runs_dev", "nice_band_tables_dev", "nice_band_pack_bits",
     "nice_band_assemble", "nice_tile_pixels",
     "nice_pipe_create", "nice_pipe_destroy", "nice_pipe_stream_stride", "nice_pipe_encode",
-    "nice_pipe_decode",
+    "nice_pipe_decode", "nice_pipe_set_checksums",
 ]
 
 
@@ -97,6 +97,8 @@ def lib():
                                         ctypes.c_uint8, ctypes.c_uint8, u8p, u64, u8p]
     L.nice_decode_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u64, u8p, u32, u32,
                                         u32, ctypes.c_uint8, u8p, u64, u32, u8p]
+    L.nice_decode_batch_dev_hl.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u64, u8p, ctypes.c_void_p, u32,
+                                           u32, u32, ctypes.c_uint8, u8p, u64, u32, u8p]
     L.nice_pipe_create.argtypes = [ctypes.c_int, u32, u32, ctypes.c_uint8, u32, u32,
                                    ctypes.POINTER(ctypes.c_void_p)]
     L.nice_pipe_destroy.argtypes = [ctypes.c_void_p]
@@ -106,6 +108,7 @@ def lib():
                                    ctypes.c_void_p, u64, ctypes.c_void_p]
     L.nice_pipe_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u32,
                                    ctypes.c_uint8, ctypes.c_void_p, u32, ctypes.c_void_p]
+    L.nice_pipe_set_checksums.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.nice_subblock_positions_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, u32, u32, u64, u64,
                                               ctypes.c_void_p]
     _lib = L
@@ -262,19 +265,42 @@ def encode_batch(px, width: int, height: int, channels: int, out, out_len,
 
 
 def decode_batch(streams, stream_len, width: int, height: int, out_channels: int, px, status,
-                 flags: int = DEC_ALPHA_FILL_FF, stream=None, ctx: "_Ctx | None" = None) -> None:
+                 flags: int = DEC_ALPHA_FILL_FF, stream=None, ctx: "_Ctx | None" = None,
+                 host_len=None) -> None:
     """Decode ``streams`` (uint8 cuda [n, stride]) with byte lengths ``stream_len``
     (int64 cuda [n]) into ``px`` (uint8 cuda [n, >= W*H*out_channels]); per-frame
-    status codes into ``status`` (int32 cuda [n])."""
+    status codes into ``status`` (int32 cuda [n]).  Asynchronous: returns once
+    the work is queued.  ``host_len`` (the same lengths on the host: a sequence,
+    numpy array or CPU tensor) spares the call its one device read (the lengths
+    size the scratch), so it never waits for earlier work on the stream."""
     import torch
     dev = streams.device.index or 0
     n = streams.shape[0]
     st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream_ptr(torch, streams.device)
-    rc = lib().nice_decode_batch_dev(
-        (ctx or _ctx(dev)).ptr, st, ctypes.c_void_p(streams.data_ptr()), streams.stride(0),
-        ctypes.c_void_p(stream_len.data_ptr()), n, width, height, out_channels,
-        ctypes.c_void_p(px.data_ptr()), px.stride(0), flags, ctypes.c_void_p(status.data_ptr()))
+    args = ((ctx or _ctx(dev)).ptr, st, ctypes.c_void_p(streams.data_ptr()), streams.stride(0),
+            ctypes.c_void_p(stream_len.data_ptr()))
+    tail = (n, width, height, out_channels, ctypes.c_void_p(px.data_ptr()), px.stride(0), flags,
+            ctypes.c_void_p(status.data_ptr()))
+    if host_len is None:
+        rc = lib().nice_decode_batch_dev(*args, *tail)
+    else:
+        hl = (ctypes.c_uint64 * n)(*[int(x) for x in host_len])
+        rc = lib().nice_decode_batch_dev_hl(*args, ctypes.cast(hl, ctypes.c_void_p), *tail)
     _check(rc, "nice_decode_batch_dev")
+
+
+def checksum64(buf) -> int:
+    """nice_checksum64 (include/nice.h) of a byte buffer, on the host."""
+    import numpy as np
+    b = np.frombuffer(bytes(buf), np.uint8) if not hasattr(buf, "dtype") else np.asarray(buf, np.uint8).reshape(-1)
+    pad = (-b.size) % 4
+    if pad:
+        b = np.concatenate([b, np.zeros(pad, np.uint8)])
+    w = b.view("<u4").astype(np.uint64)
+    with np.errstate(over="ignore"):
+        A = int(w.sum(dtype=np.uint64))
+        B = int((w * np.arange(1, w.size + 1, dtype=np.uint64)).sum(dtype=np.uint64))
+    return (A + 0x9E3779B97F4A7C15 * B) % (1 << 64)
 
 
 # ---- streamed host pipeline (config 5: H2D / compute / D2H overlapped) ------
@@ -313,10 +339,29 @@ class Pipeline:
         except Exception:
             pass
 
+    def checksums(self, on: bool = True):
+        """From the next call on, encode / decode also record each frame's
+        checksum64 (computed on the device; ``last_sums`` after the call)."""
+        self._ck = on
+
+    def _sums(self, n, enc):
+        if not getattr(self, "_ck", False):
+            return None
+        buf = (ctypes.c_uint64 * max(n, 1))()
+        _check(lib().nice_pipe_set_checksums(self.ptr, buf if enc else None, None if enc else buf),
+               "nice_pipe_set_checksums")
+        return buf
+
+    def _sums_done(self, buf, n):
+        if buf is not None:
+            lib().nice_pipe_set_checksums(self.ptr, None, None)
+            self.last_sums = [int(buf[i]) for i in range(n)]
+
     def encode(self, frames, outs, channels_out: int | None = None):
         """frames[f] -> outs[f] (host buffers of >= stream_stride bytes); returns
         the stream lengths."""
         n = len(frames)
+        sums = self._sums(n, True)
         src = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(f) for f in frames])
         dst = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(o) for o in outs])
         caps = [o.numel() if hasattr(o, "numel") else len(o) for o in outs]
@@ -324,6 +369,7 @@ class Pipeline:
         co = self.channels if channels_out is None else channels_out
         _check(lib().nice_pipe_encode(self.ptr, src, n, co, dst, min(caps) if caps else 0, lens),
                "nice_pipe_encode")
+        self._sums_done(sums, n)
         return [int(lens[i]) for i in range(n)]
 
     def decode(self, streams, lengths, outs, out_channels: int | None = None,
@@ -332,12 +378,14 @@ class Pipeline:
         returns the per-frame statuses.  A frame's error raises NiceError unless
         raise_on_error is False (outs[f] is undefined where status[f] != 0)."""
         n = len(streams)
+        sums = self._sums(n, False)
         src = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(s) for s in streams])
         dst = (ctypes.c_void_p * max(n, 1))(*[_host_ptr(o) for o in outs])
         ln = (ctypes.c_uint64 * max(n, 1))(*lengths)
         status = (ctypes.c_int32 * max(n, 1))()
         oc = self.channels if out_channels is None else out_channels
         rc = lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status)
+        self._sums_done(sums, n)
         st = [int(status[i]) for i in range(n)]
         if rc != 0 and (raise_on_error or rc not in st):
             _check(rc, "nice_pipe_decode")

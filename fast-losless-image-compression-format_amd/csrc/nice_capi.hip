@@ -464,13 +464,16 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
 namespace {
 struct DecLayout {
   size_t total;
-  size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_rowbuf;
+  size_t o_tables, o_dstart, o_entry, o_last, o_ck, o_cpx, o_cstart, o_recs, o_changed, o_fchanged, o_rowbuf;
   size_t o_ev, o_evck, o_evn, o_agree, o_items, o_icount;
   size_t o_hand, o_abort;
 };
-// Jacobi iterations queued before the host first checks for the fixpoint (one
-// change flag each); further iterations, if any, check after every launch.
-constexpr uint32_t kSyncQueued = 6, kSyncFlags = 8;
+// Jacobi iterations queued (one change flag each; each returns at once when the
+// previous one changed nothing), then the device-side settle (dec_sync_settle)
+// and one more iteration behind its flag: no host round trip.  Flags: the
+// queued iterations', the settle's, the last iteration's.
+constexpr uint32_t kSyncQueued = 8, kSyncFlags = kSyncQueued + 2;
+constexpr uint32_t kSettledFlag = kSyncQueued, kFinalFlag = kSyncQueued + 1;
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf,
                      uint32_t ev_cap, uint32_t subs, size_t hand = 0) {
   DecLayout L{};
@@ -485,6 +488,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_cstart = take((size_t)n_frames * max_chunks * 8);
   L.o_recs = take((size_t)n_frames * ((npx + 3) & ~3ull) * 4);
   L.o_changed = take(4 * kSyncFlags);
+  L.o_fchanged = take((size_t)n_frames * 4);
   L.o_rowbuf = take(rowbuf);
   // first-pass pixel events (ev_cap per slice, 0: not kept)
   L.o_ev = take((size_t)n_frames * ((max_chunks + 63) & ~63u) * ev_cap * 4);
@@ -579,6 +583,15 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                                  out_channels, d_px, px_stride, flags, d_status);
 }
 
+int nice_decode_batch_dev_hl(nice_ctx* ctx, void* stream, const uint8_t* d_streams, uint64_t stream_stride,
+                             const uint64_t* d_stream_len, const uint64_t* h_stream_len, uint32_t n_frames,
+                             uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px, uint64_t px_stride,
+                             uint32_t flags, int32_t* d_status) {
+  if (n_frames && !h_stream_len) return NICE_E_ARG;
+  return nice::decode_batch_impl(ctx, stream, d_streams, stream_stride, d_stream_len, h_stream_len, n_frames, w, h,
+                                 out_channels, d_px, px_stride, flags, d_status);
+}
+
 }  // extern "C"
 
 // h_stream_len: the lengths on the host when the caller has them (saves a
@@ -586,7 +599,7 @@ int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
 int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_streams, uint64_t stream_stride,
                             const uint64_t* d_stream_len, const uint64_t* h_stream_len, uint32_t n_frames,
                             uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px, uint64_t px_stride,
-                            uint32_t flags, int32_t* d_status, uint32_t* h_unsettled) {
+                            uint32_t flags, int32_t* d_status) {
   if (!ctx || !d_streams || !d_stream_len || !d_status) return NICE_E_ARG;
   if (out_channels != 3 && out_channels != 4) return NICE_E_ARG;
   if ((stream_stride & 3) || ((uintptr_t)d_streams & 3)) return NICE_E_ARG;
@@ -751,39 +764,31 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   hipLaunchKernelGGL(dec_init_entries, dim3((max_chunks + 255) / 256 < 64 ? (max_chunks + 255) / 256 : 64, n_frames),
                      dim3(256), 0, st, a);
   const dim3 cgrid(n_frames * a.chunk_blocks);
-  // Jacobi iteration of the chunk entry states to the fixpoint
-  // (the first kSyncQueued launches go out without host round trips: each one
-  // returns at once if the previous one changed nothing)
-  uint32_t host_changed = 1;
+  // Jacobi iteration of the chunk entry states to the fixpoint, all on the
+  // device: queued iterations (each returns at once if the previous one changed
+  // nothing), the sequential settle of frames still changing after the last
+  // one, and one more iteration for the slices the settle moved
   uint32_t it_count = 0;
-  const uint32_t max_it = max_chunks + 2;
-  uint32_t queued = std::min(kSyncQueued, max_it);
+  uint32_t queued = std::min(kSyncQueued, max_chunks + 1);
   if (const char* ev = getenv("NICE_DEC_SYNC_QUEUED")) {   // tests: fewer queued iterations
     const uint32_t v = (uint32_t)atoi(ev);
     if (v >= 1 && v < queued) queued = v;
   }
+  uint32_t* fchanged = (uint32_t*)(base + L.o_fchanged);
   NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
+  NICE_HIP(hipMemsetAsync(fchanged, 0, (size_t)n_frames * 4, st));
   for (uint32_t it = 0; it < queued; ++it, ++it_count) {
     tm.begin(it ? NICE_PH_DEC_RESYNC : NICE_PH_DEC_SYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + it, it ? changed + it - 1 : nullptr);
+    hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + it, it ? changed + it - 1 : nullptr,
+                       it + 1 == queued ? fchanged : nullptr);
     tm.end(st);
   }
-  if (h_unsettled) {
-    // no host round trip: the caller checks the flag once the stream is done
-    NICE_HIP(hipMemcpyAsync(h_unsettled, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
-    host_changed = 0;
-  } else {
-    NICE_HIP(hipMemcpyAsync(&host_changed, changed + queued - 1, 4, hipMemcpyDeviceToHost, st));
-    NICE_HIP(hipStreamSynchronize(st));
-  }
-  for (uint32_t it = queued; host_changed && it < max_it; ++it, ++it_count) {
-    NICE_HIP(hipMemsetAsync(changed + kSyncFlags - 1, 0, 4, st));
-    tm.begin(NICE_PH_DEC_RESYNC, st);
-    hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + kSyncFlags - 1, nullptr);
-    tm.end(st);
-    NICE_HIP(hipMemcpyAsync(&host_changed, changed + kSyncFlags - 1, 4, hipMemcpyDeviceToHost, st));
-    NICE_HIP(hipStreamSynchronize(st));
-  }
+  tm.begin(NICE_PH_DEC_RESYNC, st);
+  hipLaunchKernelGGL(dec_sync_settle, dim3(n_frames), dim3(64), 0, st, a, changed + queued - 1, fchanged,
+                     changed + kSettledFlag);
+  hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + kFinalFlag,
+                     changed + kSettledFlag, nullptr);
+  tm.end(st);
   // the last sync iteration (no entry changed) already produced chunk_px
   tm.begin(NICE_PH_DEC_SCAN, st);
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);

@@ -640,7 +640,9 @@ __device__ __forceinline__ uint32_t ev_pack(uint32_t pfx, uint32_t s0, uint32_t 
 // `prev`: the previous iteration's change flag -- when it is 0 the entries are
 // at the fixpoint already and this launch does nothing (the host queues several
 // iterations without waiting for each).
-__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev) {
+// `fchanged` (optional): per-frame change flags, for dec_sync_settle.
+__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev,
+                                                              uint32_t* fchanged) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
   if (prev && *prev == 0) return;
@@ -799,8 +801,66 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
     if (a.entry[base + j + 1] != x) {
       a.entry[base + j + 1] = x;
       atomicOr(changed, 1u);
+      if (fchanged) fchanged[f] = 1u;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// D1b: the fixpoint on the device.  After the queued Jacobi iterations, a frame
+// whose entries still changed in the last one (fchanged) gets them by one
+// sequential parse: lane 0 of the frame's wave walks its slices in order, each
+// from the previous slice's exit, with the same stop rule as dec_sync (slice
+// end, stream end + 64 bits, more pixels than the frame), and writes every
+// entry.  A dec_sync launch after this one (prev = *settled) re-parses the
+// slices whose entries moved, which brings their pixel counts, checkpoints and
+// meeting points up to date; its exits then equal the entries.  Self-
+// synchronisation settles ordinary streams within two or three iterations, so
+// this is a bound on pathological ones, not a path streams normally take --
+// and it replaces the host's fixpoint check, so the call never waits.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void dec_sync_settle(DecArgs a, const uint32_t* last_changed,
+                                                      const uint32_t* fchanged, uint32_t* settled) {
+  __shared__ LutLds S;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[64 * RING_STRIDE];
+  const uint32_t f = blockIdx.x;
+  if (*last_changed == 0 || fchanged[f] == 0 || a.status[f] != 0) return;
+  const uint64_t len = a.stream_len[f];
+  const uint64_t D = a.data_start[f];
+  const uint32_t nc = n_chunks(len, D, a.chunk_bits);
+  if (nc < 2) return;
+  load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
+  __syncthreads();
+  StreamParams SP;
+  SP.load(S);
+  const uint32_t lane = threadIdx.x;
+  const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const uint64_t base = (uint64_t)f * a.max_chunks;
+  const uint32_t N = a.W * a.H;
+  const unsigned long long hard = len * 8 + 64;
+  const uint32_t* my = ring + lane * RING_STRIDE;
+  Lane L;
+  L.pos = D;
+  L.rp = RING_W;
+  uint32_t dk = 0;
+  for (uint32_t j = 0; j + 1 < nc; ++j) {
+    const unsigned long long end = D + (unsigned long long)(j + 1) * a.chunk_bits;
+    uint32_t px = 0;
+    bool active = lane == 0;
+    for (;;) {
+      if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
+      if (!__any(active)) break;
+      if (__any(active && !lane_ok(L))) ring_fill<false>(ring, p, len, al16, L);
+      if (active) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
+        px = sat_add(px, pixel_count(pfx, dk));
+      }
+    }
+    if (lane == 0) a.entry[base + j + 1] = ps_pack(L.pos - D, dk);
+  }
+  if (lane == 0) *settled = 1u;
 }
 
 // ---------------------------------------------------------------------------

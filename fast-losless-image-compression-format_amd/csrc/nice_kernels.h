@@ -217,7 +217,8 @@ constexpr uint32_t EV_OVERFLOW = 0xFFFFFFFFu, AGREE_NONE = 0xFFFFu;
 
 __global__ void dec_tables(DecArgs a);
 __global__ void dec_init_entries(DecArgs a);
-__global__ void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev);
+__global__ void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev, uint32_t* fchanged);
+__global__ void dec_sync_settle(DecArgs a, const uint32_t* last_changed, const uint32_t* fchanged, uint32_t* settled);
 __global__ void dec_scan(DecArgs a);
 __global__ void dec_strict_refill(DecArgs a);   // NICE_DEC_STRICT_REFERENCE only
 __global__ void dec_emit(DecArgs a);

@@ -97,11 +97,21 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
 /* Decode n_frames streams resident in device memory (all w x h).
  * d_streams: stream f at d_streams + f*stream_stride, d_stream_len[f] bytes.
  * d_px: frame f written at d_px + f*px_stride with out_channels (3 or 4) bytes
- * per pixel.  d_status[f] = NICE_OK or a negative code.  Asynchronous. */
+ * per pixel.  d_status[f] = NICE_OK or a negative code.  Asynchronous: the
+ * parse fixpoint is reached on the device; the call reads the lengths back
+ * first (they size the scratch), i.e. waits for the work queued on `stream`
+ * before it, never for the decode itself. */
 int nice_decode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
                           uint64_t stream_stride, const uint64_t* d_stream_len, uint32_t n_frames,
                           uint32_t w, uint32_t h, uint8_t out_channels, uint8_t* d_px,
                           uint64_t px_stride, uint32_t flags, int32_t* d_status);
+/* The same with the lengths also on the host (h_stream_len[f] == d_stream_len[f]):
+ * the call only enqueues work, it never waits for the device. */
+int nice_decode_batch_dev_hl(nice_ctx* ctx, void* stream, const uint8_t* d_streams,
+                             uint64_t stream_stride, const uint64_t* d_stream_len,
+                             const uint64_t* h_stream_len, uint32_t n_frames, uint32_t w, uint32_t h,
+                             uint8_t out_channels, uint8_t* d_px, uint64_t px_stride, uint32_t flags,
+                             int32_t* d_status);
 
 /* ---- one image sharded over ranks (config 4) ----
  * The image's raster is cut into bands of whole encoder tiles (1024 pixels in
@@ -177,11 +187,18 @@ int nice_pipe_encode(nice_pipe* p, const uint8_t* const* px, uint32_t n_frames, 
                      uint8_t* const* out, uint64_t out_cap, uint64_t* out_len);
 /* streams[f], stream_len[f] -> px[f] (w*h*out_channels bytes, out_channels <=
  * the pipe's channels); status[f] per frame (flags as nice_decode).  Blocks.
- * px[f] is defined only where status[f] == NICE_OK: a chunk whose speculative
- * parse had not settled when it was queued is copied out first and decoded
- * again at slot reuse, so a frame that then fails may hold stale pixels. */
+ * px[f] is defined only where status[f] == NICE_OK. */
 int nice_pipe_decode(nice_pipe* p, const uint8_t* const* streams, const uint64_t* stream_len, uint32_t n_frames,
                      uint8_t out_channels, uint8_t* const* px, uint32_t flags, int32_t* status);
+/* Per-frame checksums computed on the device from what the pipe copies to the
+ * host (end-to-end checks of streamed runs whose host buffers are reused):
+ * while set, nice_pipe_encode writes enc_sums[f] = nice_checksum64 of stream f
+ * and nice_pipe_decode dec_sums[f] = that of frame f's pixels (either pointer
+ * may be null; each must hold n_frames entries of the calls that follow).
+ * nice_checksum64 of n bytes: zero-pad to whole little-endian u32 words w_i,
+ * A = sum w_i, B = sum (i + 1) w_i (mod 2^64), checksum = A + 0x9E3779B97F4A7C15 B
+ * (mod 2^64). */
+int nice_pipe_set_checksums(nice_pipe* p, uint64_t* enc_sums, uint64_t* dec_sums);
 
 /* ---- command-line front end helper (host only) ----
  * Reverses the PNG scanline filters (types 0-4) of h rows of w pixels of bpp

@@ -73,3 +73,21 @@ def test_cpp_mirror_roundtrip(tmp_path, O):
     assert out.stdout.startswith("ok")
     # the example's frame is NICE-SYN-v1 seed 1: its stream is the oracle's
     assert open(path, "rb").read() == O.encode(O.gen_syn_v1(1283, 719, 4, 1), 1283, 719, 4)
+
+
+def test_checksum64_definition():
+    """checksum64 (include/nice.h, nice_pipe_set_checksums) against its
+    definition written out word by word, odd lengths zero-padded."""
+    pkg = nice_pkg()
+    import numpy as np
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 3, 4, 5, 17, 1001):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        p = b + bytes(-n % 4)
+        A = B = 0
+        for i in range(len(p) // 4):
+            wv = int.from_bytes(p[4 * i:4 * i + 4], "little")
+            A += wv
+            B += (i + 1) * wv
+        want = (A + 0x9E3779B97F4A7C15 * B) % (1 << 64)
+        assert pkg.checksum64(b) == want, n

@@ -62,8 +62,9 @@ def test_pipe_bad_stream_status(nice, O):
 
 def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
     """One queued sync iteration per chunk: the parse of long slices has not
-    settled when the chunk's kernels are queued, so the pipeline must detect it
-    at slot reuse and decode the chunk again (blocking) -- exact pixels."""
+    settled after it, so the device settle (dec_sync_settle: a sequential parse
+    of the frames still changing) and the iteration behind it must give the
+    fixpoint -- exact pixels, no host check."""
     monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
     w, h, c, n = 640, 480, 4, 9
     frames = _frames(O, n, w, h, c, seed0=40)
@@ -78,8 +79,8 @@ def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
 
 
 def test_pipe_decode_unsettled_with_bad_stream(nice, O, monkeypatch):
-    """The redo path with an error in a redone chunk: every good frame exact,
-    the bad frame's status an error (its pixels are undefined, nice.h)."""
+    """The settle path with an error in a settled chunk: every good frame
+    exact, the bad frame's status an error (its pixels are undefined, nice.h)."""
     monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
     w, h, c, n = 640, 480, 4, 5
     frames = _frames(O, n, w, h, c, seed0=60)
@@ -94,4 +95,25 @@ def test_pipe_decode_unsettled_with_bad_stream(nice, O, monkeypatch):
     for i in (0, 1, 2, 4):
         assert st[i] == 0, (i, st)
         assert np.array_equal(dec[i].reshape(-1, c)[:, :3], frames[i].reshape(-1, c)[:, :3]), i
+    p.close()
+
+
+@pytest.mark.parametrize("c", [3, 4])
+def test_pipe_checksums(nice, O, c):
+    """nice_pipe_set_checksums: the device checksum of every stream and every
+    decoded frame equals checksum64 of the bytes the pipe hands back (RGB frames
+    of odd size: unaligned device frames), while the host buffers are reused."""
+    w, h, n = 333, 77, 9
+    frames = _frames(O, n, w, h, c, seed0=70)
+    p = nice.Pipeline(w, h, c, batch=2, depth=2)
+    outs = [np.zeros(p.stream_stride, np.uint8) for _ in range(n)]
+    p.checksums(True)
+    lens = p.encode(frames, outs)
+    sums = p.last_sums
+    for i in range(n):
+        assert sums[i] == nice.checksum64(O.encode(frames[i], w, h, c)), i
+    dec = [np.zeros(w * h * c, np.uint8) for _ in range(n)]
+    assert p.decode(outs, lens, dec) == [0] * n
+    for i in range(n):
+        assert p.last_sums[i] == nice.checksum64(dec[i]), i
     p.close()
