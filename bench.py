@@ -166,6 +166,55 @@ def load_traffic(phase, frames, path=None):
     return None, None
 
 
+SQ_KERNELS = {"classify": ["nice::enc_classify_pair_m", "nice::enc_classify_pair", "nice::enc_classify_ring"],
+              "pack": ["nice::enc_pack"], "sync": ["nice::dec_sync"], "emit": ["nice::dec_emit"],
+              "rundigits": ["nice::enc_rundigits"], "place": ["nice::dec_place"], "rows": ["nice::dec_rows"]}
+
+
+def load_sq(px_per_run=32 * 3840 * 2160, path=None):
+    """VALU / SALU wave-instructions per pixel, wait share and LDS bank-conflict
+    share of the hot kernels, from the newest committed SQ counter passes
+    (profiles/pmc_sq_rNN*.txt: tools/pmc_kernel.sh, 32 4K frames per
+    dispatch); None if absent."""
+    import glob
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_sq_r*.txt")))
+        if not cands:
+            return None
+        path = cands[-1]
+    vals = {}
+    try:
+        with open(path) as fh:
+            for line in fh:
+                parts = line.split()
+                if not parts:
+                    continue
+                d = vals.setdefault(parts[0], {})
+                for kv in parts[1:]:
+                    k, _, v = kv.partition("=")
+                    try:
+                        d[k] = float(v)
+                    except ValueError:
+                        pass
+    except OSError:
+        return None
+    out = {"source": os.path.basename(path), "pixels_per_dispatch": px_per_run}
+    for name, ks in SQ_KERNELS.items():
+        d = next((vals[k] for k in ks if k in vals), None)
+        if not d or "SQ_INSTS_VALU" not in d:
+            continue
+        e = {"kernel": next(k for k in ks if k in vals),
+             "valu_per_px": round(d["SQ_INSTS_VALU"] / px_per_run, 3)}
+        if "SQ_INSTS_SALU" in d:
+            e["salu_per_px"] = round(d["SQ_INSTS_SALU"] / px_per_run, 3)
+        if d.get("SQ_ACTIVE_INST_ANY"):
+            e["wait_share"] = round(d.get("SQ_WAIT_INST_ANY", 0.0) / d["SQ_ACTIVE_INST_ANY"], 3)
+        if d.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_conflict_share"] = round(d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_LDS_IDX_ACTIVE"], 3)
+        out[name] = e
+    return out
+
+
 def sharded_image(torch, nice, dist, device, side, rank, world, reps=3):
     """BASELINE config 4: one side x side RGBA image encoded by all ranks
     (bands + RCCL exchanges, fast-losless-image-compression-format_amd/sharded.py)."""
@@ -699,6 +748,7 @@ def main():
                      "traffic": traffic,
                      "traffic_ratio": round(traffic / algo[dom], 3) if traffic else None,
                      "traffic_source": traffic_src,
+                     "sq_counters": load_sq(),
                      "algo_bytes_per_launch": algo[dom],
                      "avg_launch_ms": round(avg_s * 1e3, 4)},
         # whole path against HBM: encode (px in + stream out) + decode (stream in + px out)

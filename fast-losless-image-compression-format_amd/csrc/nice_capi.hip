@@ -310,9 +310,11 @@ static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, u
 // The classify kernel for a frame shape (every kernel writes the same
 // records, histogram and tile edges): the LDS ring (each pixel loaded once)
 // wherever the rows fit it, the strip kernel for wider RGBA rows of whole
-// tiles, the round-1 window kernel otherwise.  `aligned`: the pixel base
-// (frames: and stride) is 4-byte aligned, as the ring and strip loads need.
-enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR };
+// tiles, per-tile row windows for every other wide shape, and the round-1
+// window kernel for pixel memory that is not 4-byte aligned.  `aligned`: the
+// pixel base (frames: and stride) is 4-byte aligned, as the ring, strip and
+// tile-window loads need.
+enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR, CLS_K_TWIN };
 static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
   if (w < 3) return CLS_K_TINY;
   if (!aligned || getenv("NICE_ENC_NO_RING")) return CLS_K_WINDOW;
@@ -321,7 +323,7 @@ static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
   if (w <= CLS_RING_MAX_W) return CLS_K_RING;
   if (channels == 4 && w % ENC_TILE == 0) return CLS_K_STRIP;
   if (w <= CLS_RING2_MAX_W) return CLS_K_RING2;
-  return CLS_K_WINDOW;
+  return CLS_K_TWIN;   // per-tile row windows: any wider shape
 }
 // Launches it over `work` tiles (frames x band tiles); rows_total: the rows the
 // strip kernel walks per frame.
@@ -366,6 +368,14 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
     case CLS_K_TINY:
       hipLaunchKernelGGL(enc_classify_tiny, dim3((uint32_t)blocks), dim3(256), 0, st, a);
       break;
+    case CLS_K_TWIN: {
+      const uint64_t tb = 2ull * ctx->cus, tper = (work + tb - 1) / tb;
+      a.tiles_per_block = (uint32_t)tper;
+      const dim3 g((uint32_t)((work + tper - 1) / tper));
+      if (rgb) hipLaunchKernelGGL(a.cmask ? enc_classify_twin3_m : enc_classify_twin3, g, dim3(CLS_THREADS_HOST), 0, st, a);
+      else hipLaunchKernelGGL(a.cmask ? enc_classify_twin_m : enc_classify_twin, g, dim3(CLS_THREADS_HOST), 0, st, a);
+      break;
+    }
     default:
       hipLaunchKernelGGL(enc_classify, dim3((uint32_t)blocks), dim3(256), 0, st, a);
   }

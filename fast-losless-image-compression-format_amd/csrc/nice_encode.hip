@@ -1377,6 +1377,180 @@ __device__ __forceinline__ void enc_classify_strip_body(const EncArgs& a) {
     if (v) atomicAdd(&a.hist[(uint64_t)f * N_BINS + k], v);
   }
 }
+// ---------------------------------------------------------------------------
+// K1w: classify with per-tile row windows (rows too wide for any ring and not
+// whole tiles per strip row: RGBA with W > CLS_RING2_MAX_W and W % 1024 != 0,
+// RGB with W > CLS_RING2_MAX_W).  Each block walks a contiguous tile range
+// like the ring kernels; for each tile it stages four LINEAR windows,
+// window r = pixels [start - rW - 3, start - rW + 1027) in Y space, so every
+// reference of the tile's pixels (0..3 rows back, 3 pixels either side,
+// wrapping across row ends as code.rs:141-145's linear offsets do) is inside
+// the window of its row offset.  Rows above are read from HBM/L2 once per
+// window (4 B/px more than the ring's single read); the next tile's windows
+// load into registers while this one is classified.  The mode decision is the
+// ring kernels' classify_y over explicit window bases.
+// ---------------------------------------------------------------------------
+constexpr int TW_RS = ENC_TILE + 8;                                         // window words
+constexpr int TW_LD = (ENC_TILE + 6 + CLS_THREADS - 1) / CLS_THREADS;       // loads per window per thread (3)
+
+template <int C, bool MASK_OUT>
+__device__ __forceinline__ void enc_classify_twin_body(const EncArgs& a) {
+  __shared__ uint32_t win[4][TW_RS];
+  __shared__ uint32_t hs[C0_N + 2 * SX_N];
+  __shared__ uint32_t run_hist[8];
+  __shared__ uint32_t mask[ENC_TILE / 32];
+  __shared__ uint32_t ltab[CLS_PPT][16];
+  const uint64_t total_work = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
+  const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
+  const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
+  if (w_begin >= w_end) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t cbr = (C0_BR << 3) | rec2_abs((uint32_t)lane), csd = (C0_SD << 3) | rec2_abs((uint32_t)lane);
+  const uint32_t cunc = rec2_unc((uint32_t)lane);
+  const uint32_t W = a.W;
+  const int64_t N = (int64_t)W * a.H;
+  for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+  if (tid < 8) run_hist[tid] = 0;
+  // luma reference k of slot q's thread 0: window lr_rows(k), column q * 512 + 3 - lr_px(k)
+  if (tid < 16 * CLS_PPT) {
+    const int q = tid >> 4, k = tid & 15;
+    ltab[q][k] = k < 11 ? (uint32_t)(lr_rows(k) * TW_RS + q * CLS_THREADS + 3 - lr_px(k)) : 0u;
+  }
+  auto flush = [&](uint32_t frame) {
+    __syncthreads();
+    for (int b = tid; b < N_BINS; b += CLS_THREADS) {
+      uint32_t v = slot_hist_bin(hs, b);
+      if (b >= BIN_PREFIX + P_RUN1 && b < BIN_PREFIX + P_RUN1 + 8) v += run_hist[b - BIN_PREFIX - P_RUN1];
+      if (v) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], v);
+    }
+    __syncthreads();
+    for (int b = tid; b < (int)(C0_N + 2 * SX_N); b += CLS_THREADS) hs[b] = 0;
+    if (tid < 8) run_hist[tid] = 0;
+  };
+  // the tile's four windows into registers (0 outside the frame / the band's pixel memory)
+  uint32_t pw[4][TW_LD];
+  auto fetch = [&](const TileIter& ti) {
+    const uint8_t* fr = a.px + (uint64_t)ti.f * a.frame_stride;
+    const int64_t start = (int64_t)ti.tt() * ENC_TILE;
+    const int64_t lo = max((int64_t)0, a.px_lo), hi = min(N, a.px_hi);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < TW_LD; ++k) {
+        const int c = tid + k * CLS_THREADS;
+        const int64_t g = start - (int64_t)r * W - 3 + c;
+        pw[r][k] = (c < ENC_TILE + 6 && g >= lo && g < hi) ? px_word<C>(fr, g) : 0u;
+      }
+  };
+  TileIter it(a, w_begin), nx(a, w_begin);
+  uint32_t cur_frame = it.f;
+  fetch(nx);
+  nx.step(1);
+  for (uint64_t w = w_begin; w < w_end; ++w, it.step(1)) {
+    const uint32_t f = it.f;
+    if (f != cur_frame) {
+      flush(cur_frame);
+      cur_frame = f;
+    }
+    const int64_t start = (int64_t)it.tt() * ENC_TILE;
+    const int count = (int)min((int64_t)ENC_TILE, N - start);
+    __syncthreads();   // the previous tile's readers are done with the windows
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < TW_LD; ++k) {
+        const int c = tid + k * CLS_THREADS;
+        if (c < ENC_TILE + 6) win[r][c] = y_from_rgba(pw[r][k]);
+      }
+    if (w + 1 < w_end) fetch(nx);
+    nx.step(1);
+    __syncthreads();
+    // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
+    uint32_t coded_bits = 0;
+    unsigned long long wbal[CLS_PPT];
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const int64_t i = start + p;
+      const bool coded = p < count && (i == 0 || win[0][p + 3] != win[0][p + 2]);
+      const unsigned long long bal = __ballot(coded);
+      wbal[q] = bal;
+      if (lane == 0) {
+        const int wb = (q * CLS_THREADS + (tid & ~63)) >> 5;
+        mask[wb] = (uint32_t)bal;
+        mask[wb + 1] = (uint32_t)(bal >> 32);
+        if constexpr (MASK_OUT) {
+          uint32_t* cm = a.cmask + it.tile() * (ENC_TILE / 32);
+          cm[wb] = (uint32_t)bal;
+          cm[wb + 1] = (uint32_t)(bal >> 32);
+        }
+      }
+      coded_bits |= (coded ? 1u : 0u) << q;
+    }
+    __syncthreads();
+    if (tid < 64) {   // first / last coded pixel of the tile
+      const uint32_t mw = tid < ENC_TILE / 32 ? mask[tid] : 0u;
+      const unsigned long long nz = __ballot(mw != 0);
+      if (tid == 0) {
+        const uint64_t t = it.tile();
+        uint32_t first = NONE, last = NONE;
+        if (nz) {
+          const int fw = __builtin_ctzll(nz), lw = 63 - __builtin_clzll(nz);
+          first = (uint32_t)(start + fw * 32 + __builtin_ctz(mask[fw]));
+          last = (uint32_t)(start + lw * 32 + 31 - __builtin_clz(mask[lw]));
+        }
+        a.tile_first[t] = first;
+        a.tile_last[t] = last;
+      }
+    }
+    const bool fast = start >= 3 * (int64_t)W + 3;
+    uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + start;
+    uint32_t rec[CLS_PPT];
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      const uint32_t* b0 = &win[0][p];
+      const uint32_t* b1 = &win[1][p];
+      const uint32_t* b2 = &win[2][p + 3];
+      const uint32_t* b3 = &win[3][p];
+      uint32_t rf;
+      if (fast)   // block-uniform
+        rf = classify_y<false>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, 0u, ltab[q], cbr, csd, b0[3]);
+      else
+        rf = classify_y<true>(b0, b1, b2, b3, &win[0][0], (uint32_t)tid, W, (uint32_t)(start + p), nullptr, cbr,
+                              csd, b0[3]);
+      rec[q] = coded ? rf : cunc;
+    }
+#pragma unroll
+    for (int q = 0; q < CLS_PPT; ++q) {
+      const int p = q * CLS_THREADS + tid;
+      const bool coded = (coded_bits >> q) & 1u;
+      if (p < count) recs[p] = rec[q];
+      slot_hist_add(hs, rec[q]);
+      if constexpr (MASK_OUT) continue;   // enc_rundigits counts them
+      const bool next_coded = lane < 63 && ((wbal[q] >> (lane + 1)) & 1ull);
+      if (coded && !next_coded) {
+        const unsigned long long above = lane < 63 ? (wbal[q] >> (lane + 1)) : 0ull;
+        const int nxp = above ? p + 1 + (int)__builtin_ctzll(above) : next_coded_local(mask, p | 63);
+        if (nxp < count && nxp > p + 1) {
+          uint32_t mm = (uint32_t)(nxp - p - 2);
+          while (true) {
+            atomicAdd(&run_hist[mm & 7u], 1u);
+            if (mm < 8) break;
+            mm >>= 3;
+          }
+        }
+      }
+    }
+  }
+  flush(cur_frame);
+}
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_twin(EncArgs a) { enc_classify_twin_body<4, false>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_twin_m(EncArgs a) { enc_classify_twin_body<4, true>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_twin3(EncArgs a) { enc_classify_twin_body<3, false>(a); }
+__global__ __launch_bounds__(CLS_THREADS) void enc_classify_twin3_m(EncArgs a) { enc_classify_twin_body<3, true>(a); }
+
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip(EncArgs a) { enc_classify_strip_body<false>(a); }
 // frames: the tiles' coded flags out, run digits by enc_rundigits
 __global__ __launch_bounds__(CLS_THREADS) void enc_classify_strip_m(EncArgs a) { enc_classify_strip_body<true>(a); }

@@ -103,6 +103,11 @@ __global__ void enc_classify_ring3_m(EncArgs a);
 __global__ void enc_classify_ring2_m(EncArgs a);
 __global__ void enc_classify_ring2_3_m(EncArgs a);
 __global__ void enc_rundigits(EncArgs a);
+// per-tile row windows (any W > CLS_RING2_MAX_W the strip kernel does not take; RGBA and RGB)
+__global__ void enc_classify_twin(EncArgs a);
+__global__ void enc_classify_twin_m(EncArgs a);
+__global__ void enc_classify_twin3(EncArgs a);
+__global__ void enc_classify_twin3_m(EncArgs a);
 constexpr uint32_t CLS_PAIR_MAX_W = 4095;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
 constexpr uint32_t DEC_PARSE_THREADS = 512;

@@ -1,8 +1,9 @@
 """Classify kernel routing: every frame shape the reference encodes the same
 way (code.rs:141-145, 159-414) goes through an LDS-staged kernel where the
 rows fit -- the 16K-pixel ring (W <= 4777), the strip kernel (RGBA, W % 1024
-== 0), the 32K-pixel ring (W <= 10239: 8K UHD's 7680, RGB rows) -- including
-the band API (config 4) at ring widths.  Streams must equal the oracle's and
+== 0), the 32K-pixel ring (W <= 10239: 8K UHD's 7680, RGB rows), per-tile
+row windows for every wider shape (RGB, or RGBA rows that are not whole
+tiles) -- including the band API (config 4).  Streams must equal the oracle's and
 the test hook must name the fast kernel."""
 import ctypes
 
@@ -11,7 +12,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-WINDOW, TINY, RING, RING2, STRIP, PAIR = range(6)
+WINDOW, TINY, RING, RING2, STRIP, PAIR, TWIN = range(7)
 
 
 def _same(got, want, what):
@@ -41,7 +42,8 @@ def _encode_dev(nice, px, w, h, c, ctx):
 @pytest.mark.parametrize("shape,kind", [((7680, 64, 4), RING2), ((6000, 32, 3), RING2), ((10239, 9, 4), RING2),
                                         ((10239, 11, 3), RING2), ((4777, 20, 4), RING), ((4778, 20, 3), RING2),
                                         ((4095, 20, 4), PAIR), ((4095, 20, 3), RING), ((1000, 30, 4), PAIR),
-                                        ((8192, 12, 4), STRIP), ((10240, 5, 3), WINDOW), ((11000, 5, 4), WINDOW)],
+                                        ((8192, 12, 4), STRIP), ((10240, 5, 3), TWIN), ((11000, 5, 4), TWIN),
+                                        ((10241, 9, 3), TWIN), ((12000, 7, 4), TWIN), ((20000, 5, 3), TWIN)],
                          ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
 def test_route_and_bitexact(nice, O, shape, kind):
     w, h, c = shape
@@ -70,7 +72,8 @@ def test_8k_uhd_batch(nice, O):
 
 
 @pytest.mark.parametrize("shape,kind", [((1920, 1080, 4, 4), PAIR), ((1000, 700, 3, 3), RING),
-                                        ((7680, 300, 4, 3), RING2), ((8192, 200, 4, 2), STRIP)],
+                                        ((7680, 300, 4, 3), RING2), ((8192, 200, 4, 2), STRIP),
+                                        ((11000, 60, 4, 3), TWIN), ((10300, 50, 3, 2), TWIN)],
                          ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
 def test_band_routes(nice, O, shape, kind):
     """The band API's classify takes the same kernels (a band's first block
