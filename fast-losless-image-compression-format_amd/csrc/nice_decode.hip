@@ -2276,6 +2276,340 @@ __global__ __launch_bounds__(1024) void dec_rows_wide(DecArgs a) { dec_rows_body
 __global__ __launch_bounds__(512) void dec_rows8(DecArgs a) { dec_rows_body<512, true, 8>(a); }
 
 // ---------------------------------------------------------------------------
+// D5d: dataflow row reconstruction for small batches (round 5; 64 <= W <=
+// 4096, one frame per block, frames <= CUs).  dec_rows keeps every wave of a
+// block on one row: a block barrier after the speculative pass, two per fix-up
+// round, one after the emit, and the record pre-pass and the raster stores on
+// the row's critical path.  At one frame per CU (single frames, config 3,
+// small RGB batches) that path sets the decode time: 2160 rows of ~6.8 us for
+// 4K.  Here the block's waves form K groups of WPR = ceil(segments / 64)
+// waves; group g reconstructs rows g, g + K, ..., so rows overlap, and the
+// waves synchronise only through LDS stamps (row + 1):
+//   fin[slot][w]  wave w's segments of the row are final in the ring;
+//   tst[slot][w]  the last three pixels of wave w's last segment are exact
+//                 (tail[slot][w]): the next wave's first lane can fix up;
+//   hst[slot]     the row's first three pixels (W_CUR references of the
+//                 row's last columns, code.rs:141-145: offsets W-1, W-3 reach
+//                 into the current row).
+// Wave w of row y waits for row y-1's waves w-1..w+1 (the references reach
+// +-3 pixels, rows 1..3 back: rows y-2, y-3 are final by induction), wave 0
+// for all of row y-1 (its entry is the row's last pixels, code.rs:412-413),
+// the last wave also for row y-1's wave 0 (right halos).  Then: pre-pass ring
+// reads (the record decode and addresses are done before the wait), the
+// speculative pass, and fix-up rounds inside the wave (lane shuffles, no
+// barriers; the first lane takes the left wave's published tail), the ring
+// row and halos, the stamp, and only then the raster stores and the next
+// rows' record loads -- off the critical path.  A ring of 8 rows (K + 3 <= 8)
+// in LDS.  Every dependency points to an earlier (row, wave) and all waves
+// are resident, so the earliest unfinished one always progresses; every wait
+// is bounded (0.2 s, then the frame fails with NICE_E_HIP and the other waves
+// stop).
+// ---------------------------------------------------------------------------
+constexpr uint32_t FLOW_THREADS = 512;
+constexpr uint32_t FLOW_SLOTS = 8;
+constexpr uint32_t FLOW_MAXW = 4;
+constexpr unsigned long long FLOW_TIMEOUT = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
+struct FlowCtl {
+  uint32_t fin[FLOW_SLOTS][FLOW_MAXW];
+  uint32_t tst[FLOW_SLOTS][FLOW_MAXW];
+  uint32_t tail[FLOW_SLOTS][FLOW_MAXW][4];
+  uint32_t hst[FLOW_SLOTS];
+  uint32_t head[FLOW_SLOTS][4];
+  uint2 rtab[FLOW_THREADS / 64][16];   // per wave: the class table of its current row
+  uint32_t zero[4];                    // the "reference" word of records that have none
+  int err;
+  uint32_t abort;
+  uint32_t pad[2];
+};
+static_assert(sizeof(FlowCtl) % 16 == 0, "ring after the control block, 16-byte aligned");
+static_assert(sizeof(FlowCtl) == FLOW_CTL_BYTES_HOST && FLOW_THREADS == FLOW_THREADS_HOST, "host LDS sizing");
+__device__ __forceinline__ uint32_t flow_peek(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// LDS-only release (the raster stores and record loads stay in flight)
+__device__ __forceinline__ void flow_publish(uint32_t* p, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void flow_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+// the wave waits until stamps[i] >= want for every bit i of mask (lanes 0..3
+// read one stamp each); false when the frame aborted or the wait timed out
+__device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, uint32_t mask, uint32_t want) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool mine = lane < FLOW_MAXW && ((mask >> lane) & 1u);
+  unsigned long long t0 = 0;
+  for (uint32_t n = 0;; ++n) {
+    const uint32_t v = mine ? flow_peek(stamps + lane) : want;
+    if (__ballot(v < want) == 0ull) break;
+    if ((n & 31u) == 0u) {
+      if (flow_peek(&C.abort)) return false;
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (n == 0) t0 = t;
+      else if (t - t0 > FLOW_TIMEOUT) {
+        atomicOr(&C.abort, 1u);
+        atomicCAS(&C.err, 0, NICE_E_HIP);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  flow_acquire();
+  return true;
+}
+__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1); }
+
+__global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
+  constexpr int S = ROWS_SEG;
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  FlowCtl& C = *reinterpret_cast<FlowCtl*>(sm);
+  constexpr uint32_t CTL_WORDS = sizeof(FlowCtl) / 4;
+  constexpr uint32_t ZERO_IDX = offsetof(FlowCtl, zero) / 4;
+  const uint32_t W = a.W, H = a.H, f = blockIdx.x;
+  const uint32_t RS = rows_ring_stride(W);
+  const uint32_t RB = CTL_WORDS + ROWS_RB;   // sm index of ring slot 0, pixel 0
+  uint32_t* const ring = sm + RB;
+  for (uint32_t i = threadIdx.x; i < CTL_WORDS; i += FLOW_THREADS) sm[i] = 0u;
+  __syncthreads();
+  if (a.status[f] != 0) return;   // block-uniform
+  const uint32_t nseg = (W + S - 1) / S, WPR = (nseg + 63) / 64, K = a.flow_k;
+  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (wid >= K * WPR) return;   // no barrier below this point
+  const uint32_t g = wid / WPR, w = wid - g * WPR, lastw = WPR - 1;
+  const uint32_t seg = w * 64u + lane;
+  const bool active = seg < nseg;
+  const uint32_t x0 = seg * S;
+  const int nvalid = active ? (int)min((uint32_t)S, W - x0) : 0;
+  const uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride;
+  uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
+  const uint32_t OC = a.out_channels;
+  const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const bool vec_rec = (W & 3u) == 0 && nvalid == S;
+  const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) ||
+                       (OC == 3 && (W & 15u) == 0 && nvalid == S);
+  const uint32_t full = (1u << WPR) - 1u;
+  const uint32_t depmask = w == 0 ? full : ((((7u << w) >> 1) & full) | (w == lastw ? 1u : 0u));
+  const bool curlane = active && x0 + S + 2u >= W;   // words that can reference row y itself (W_CUR)
+  const bool wave_cur = __any(curlane);
+  uint2* const rtab = C.rtab[wid];
+  const uint32_t lb = 17u * seg;
+  uint32_t rn[S];
+  auto load_recs = [&](uint32_t y) {
+    const uint32_t* rrow = recs + (uint64_t)y * W + x0;
+    if (vec_rec) {
+#pragma unroll
+      for (int q = 0; q < S / 4; ++q) {
+        const uint4 t = reinterpret_cast<const uint4*>(rrow)[q];
+        rn[4 * q] = t.x; rn[4 * q + 1] = t.y; rn[4 * q + 2] = t.z; rn[4 * q + 3] = t.w;
+      }
+    } else if (nvalid > 0) {
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = p < nvalid ? rrow[p] : REC_RUN;
+    } else {
+#pragma unroll
+      for (int p = 0; p < S; ++p) rn[p] = REC_RUN;
+    }
+  };
+  if (g < H) load_recs(g);
+  bool ok = true;
+  for (uint32_t y = g; y < H && ok; y += K) {
+    const uint32_t s = y & (FLOW_SLOTS - 1u), sp = (y - 1u) & (FLOW_SLOTS - 1u);
+    // ---- pre-pass, part 1 (no pixel values): the row's class table, each
+    // record's constant and kind bits, and the ring index of its reference
+    if (lane < 16) {
+      const uint32_t c = lane;
+      const unsigned long long kinds = y == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
+      const uint32_t rows = (CLS_ROWS_PACK >> (2 * c)) & 3u, dxp3 = (uint32_t)(CLS_PX_PACK >> (3 * c)) & 7u;
+      rtab[c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3,
+                           RB + ((y - rows) & (FLOW_SLOTS - 1u)) * RS + 3u - dxp3);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    uint32_t wk[S], ad[S];
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+      const uint32_t r = rec_canon(rn[p], a.rec_tag);
+      const uint32_t cls = r >> 24;   // 0..13
+      const uint2 e = rtab[cls];
+      uint32_t idx = lb + e.y + (uint32_t)p;
+      if (p < 3 || p > S - 4) idx += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
+      ad[p] = cls >= 4u ? idx : ZERO_IDX;
+      wk[p] = (e.x & 0xF0000000u) | spread3(r & 0xFFFFFFu);
+    }
+    if (curlane) {   // references past the row end into row y itself (pixels 0..2)
+#pragma unroll
+      for (int p = 0; p < S; ++p) {
+        const uint32_t r = rec_canon(rn[p], a.rec_tag);
+        const uint32_t cls = r >> 24;
+        const uint32_t tx = x0 + p + 3u - ((uint32_t)(CLS_PX_PACK >> (3u * cls)) & 7u);
+        const bool cur = cls >= 4u && ((CLS_ROWS_PACK >> (2u * cls)) & 3u) == 1u && tx >= W;
+        wk[p] = cur ? (W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8)) : wk[p];
+        ad[p] = cur ? ZERO_IDX : ad[p];
+      }
+    }
+    // ---- wait for the rows above
+    if (y > 0 && !flow_wait(C, C.fin[sp], depmask, y)) { ok = false; break; }
+    // ---- pre-pass, part 2: reference values, the row above, the entry
+    uint32_t wv[S], prev[S];
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+      const uint32_t o = sm[ad[p]];
+      wv[p] = (wk[p] & ~SP_K) | ((o + wk[p]) & SP_K);
+    }
+    uint32_t* const pr = ring + sp * RS;
+#pragma unroll
+    for (int p = 0; p < S; ++p) prev[p] = y > 0 ? pr[lb + p] : 0u;
+    IvS r0{0u, SP_K}, r1{0u, SP_K}, r2{0u, SP_K};
+    if (seg == 0) {
+      if (y == 0) {
+        r0 = r1 = r2 = ivs_exact(0u);
+      } else {
+        r0 = ivs_exact(pr[(W - 1) + ((W - 1) >> 4)]);
+        r1 = ivs_exact(pr[(W - 2) + ((W - 2) >> 4)]);
+        r2 = ivs_exact(pr[(W - 3) + ((W - 3) >> 4)]);
+      }
+    }
+    // ---- speculative pass
+    IvS v[S];
+    int lu = rows_spec<S>(v, r0, r1, r2, wv, prev);
+    bool fin = !active || lu < 0;
+    bool tex = !active || lu < S - 3;
+    if (w == 0 && lane == 0) {   // the row's first three pixels (lane 0: exact entry)
+      C.head[s][0] = v[0].lo; C.head[s][1] = v[1].lo; C.head[s][2] = v[2].lo;
+      flow_publish(&C.hst[s], y + 1u);
+    }
+    bool tpub = w == lastw;   // the last wave's tail feeds no wave
+    auto pub_tail = [&]() {
+      if (!tpub && __builtin_amdgcn_readlane((int)tex, 63)) {
+        if (lane == 63) {
+          C.tail[s][w][0] = v[S - 1].lo; C.tail[s][w][1] = v[S - 2].lo; C.tail[s][w][2] = v[S - 3].lo;
+          flow_publish(&C.tst[s][w], y + 1u);
+        }
+        tpub = true;
+      }
+    };
+    pub_tail();
+    // ---- fix-up rounds inside the wave
+    bool cur_done = !wave_cur;
+    unsigned long long t0 = 0;
+    for (uint32_t n = 0;; ++n) {
+      if (__ballot(!fin) == 0ull) break;
+      if (!cur_done && flow_peek(&C.hst[s]) >= y + 1u) {
+        flow_acquire();
+        const uint32_t h0 = C.head[s][0], h1 = C.head[s][1], h2 = C.head[s][2];
+        if (curlane) {
+#pragma unroll
+          for (int p = 0; p < S; ++p) {
+            const uint32_t k = (wv[p] >> 8) & 3u;
+            const uint32_t hv = k == 0u ? h0 : k == 1u ? h1 : h2;
+            wv[p] = (wv[p] & W_CUR) ? ((hv + (wv[p] & SP_K)) & SP_K) : wv[p];
+          }
+        }
+        cur_done = true;
+      }
+      IvS l0{shfl_up1(v[S - 1].lo), 0u}, l1{shfl_up1(v[S - 2].lo), 0u}, l2{shfl_up1(v[S - 3].lo), 0u};
+      bool lex = shfl_up1(tex ? 1u : 0u) != 0u;
+      if (lane == 0) {
+        lex = false;
+        if (w > 0 && flow_peek(&C.tst[s][w - 1]) >= y + 1u) {
+          flow_acquire();
+          l0.lo = C.tail[s][w - 1][0]; l1.lo = C.tail[s][w - 1][1]; l2.lo = C.tail[s][w - 1][2];
+          lex = true;
+        }
+      }
+      const bool go = !fin && lex && (cur_done || !curlane);
+      if (__ballot(go) != 0ull) {
+#pragma unroll
+        for (int p = 0; p < S; ++p) asm volatile("" : "+v"(wv[p]));
+        lu = rows_chain_exact<S>(v, l0, l1, l2, wv, prev, lu, go);
+        if (go) {
+          if (lu >= 0) atomicCAS(&C.err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
+          fin = true;
+          tex = true;
+        }
+        pub_tail();
+      } else {
+        // nothing to do until the left wave's tail or the row head arrive
+        if ((n & 31u) == 0u) {
+          if (flow_peek(&C.abort)) { ok = false; break; }
+          const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = t;
+          else if (t - t0 > FLOW_TIMEOUT) {
+            atomicOr(&C.abort, 1u);
+            atomicCAS(&C.err, 0, NICE_E_HIP);
+            ok = false;
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    if (!ok) break;
+    if (C.err) { atomicOr(&C.abort, 1u); ok = false; break; }
+    // ---- the ring row, its halos, the stamp
+    if (active) {
+      uint32_t* rr = ring + s * RS + lb;
+#pragma unroll
+      for (int p = 0; p < S; ++p) rr[p] = v[p].lo;   // padding pixels land in the row's spare words
+      if (seg == 0 && y > 0) {   // row y-1's right halo: this row's first three pixels
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pr[(W + k) + ((W + k) >> 4)] = v[k].lo;
+      }
+      if (x0 + S + 2u >= W) {   // row y+1's left halo: this row's last three pixels
+        uint32_t* hh = ring + ((y + 1u) & (FLOW_SLOTS - 1u)) * RS;
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+          if (p < nvalid && x0 + p + 3u >= W) hh[(int)(x0 + p - W) - 1] = v[p].lo;
+      }
+    }
+    if (lane == 0) flow_publish(&C.fin[s][w], y + 1u);
+    // ---- off the critical path: the next row's records, the raster
+    if (y + K < H) load_recs(y + K);
+    if (active) {
+      const uint64_t pix = (uint64_t)y * W + x0;
+      if (vec_out && OC == 4) {
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q)
+          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
+                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+      } else if (vec_out) {
+        uint32_t b[3 * S / 4];
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) {
+          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
+          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
+          b[3 * q] = u0 | (u1 << 24);
+          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
+          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+        }
+        uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
+#pragma unroll
+        for (int q = 0; q < 3 * S / 16; ++q) o[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+      } else if (OC == 4) {
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(outp + pix * 4);
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+          if (p < nvalid) o32[p] = unspread3(v[p].lo) | alpha;
+      } else {
+        uint8_t* o8 = outp + pix * 3;
+#pragma unroll
+        for (int p = 0; p < S; ++p) {
+          if (p < nvalid) {
+            const uint32_t u = unspread3(v[p].lo);
+            o8[3 * p] = (uint8_t)u; o8[3 * p + 1] = (uint8_t)(u >> 8); o8[3 * p + 2] = (uint8_t)(u >> 16);
+          }
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    const int e = __hip_atomic_load(&C.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (e) set_status(&a.status[f], e);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // D5c: strip-split reconstruction for wide frames: a frame's row segments are
 // cut into k strips of <= 256 lanes, one workgroup each (one per CU), all rows
 // in order.  In raster order the strip-rows ("units" (y, j)) form one chain:

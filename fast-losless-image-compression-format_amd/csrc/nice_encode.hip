@@ -482,10 +482,16 @@ constexpr int CLS_GUARD = CLS_THREADS + 8;
 // luma test offsets in Y space: R,B fields +16, G field +32, plus 256 per field
 constexpr uint32_t LUMA_KY = (256u + 16u) | ((256u + 32u) << 10) | ((256u + 16u) << 20);
 
+// (R-G, B-G) by one packed 16-bit subtract of G from the halves G<<8|R and
+// A<<8|B (borrows land in the G and A bytes, masked off), then B-G moved up by
+// one 24-bit multiply-add: 7 VALU instead of 11 for the spread-and-subtract
+// form (both checked equal over every RGB value on the host)
+typedef unsigned short nice_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t y_from_rgba(uint32_t v) {
-  const uint32_t s = spread_rgba(v);
-  const uint32_t g = (v >> 8) & 0xFFu;
-  return (s + K3(256u) - (g | (g << 20))) & K3(0xFFu);
+  const uint32_t g = __builtin_amdgcn_ubfe(v, 8, 8);
+  const nice_u16x2 d = __builtin_bit_cast(nice_u16x2, v) - __builtin_bit_cast(nice_u16x2, g | (g << 16));
+  const uint32_t t = __builtin_bit_cast(uint32_t, d);
+  return (__umul24(t & 0xFF0000u, 16u) + (t & 0xFFu)) | (g << 10);
 }
 __device__ __forceinline__ uint32_t rgb_from_y(uint32_t y) {
   // g | g << 20 as one 24-bit multiply-add (v_bfe + v_mad_u32_u24 + v_and)
@@ -933,11 +939,16 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
     const uint32_t f = ti.f;
     const int64_t start = (int64_t)ti.tt() * ENC_TILE;
     if (C == 4) {
-      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
+      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride) + start;
+      if (start + (int64_t)nti * ENC_TILE <= N) {   // block-uniform: no per-pixel bounds
 #pragma unroll
-      for (int q = 0; q < PQ; ++q) {
-        const int64_t j = start + q * CLS_THREADS + tid;
-        pf[q] = (q < 2 * nti && j < N) ? fr[j] : 0u;
+        for (int q = 0; q < PQ; ++q) pf[q] = q < 2 * nti ? fr[q * CLS_THREADS + tid] : 0u;
+      } else {
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) {
+          const int64_t j = start + q * CLS_THREADS + tid;
+          pf[q] = (q < 2 * nti && j < N) ? fr[q * CLS_THREADS + tid] : 0u;
+        }
       }
     } else {   // the iteration's dwords tid, 512 + tid, 1024 + tid
       const uint8_t* fr = a.px + (uint64_t)f * a.frame_stride;
@@ -981,13 +992,17 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
       }
     }
     uint32_t yv[PQ];   // the thread's pixels in Y space (classify's X)
+    // the mirrored guard only in iterations whose ring range starts in it or
+    // wraps (block-uniform; one iteration in eight)
+    const uint32_t k0 = (uint32_t)start & (RING - 1);
+    const bool guard = k0 < (uint32_t)CLS_GUARD || k0 + (uint32_t)(cur * ENC_TILE) > (uint32_t)RING;
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       yv[q] = y_from_rgba(pxw[q]);
       if (q < 2 * cur) {
         const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1);
         ring[k] = yv[q];
-        if (k < CLS_GUARD) ring[RING + k] = yv[q];
+        if (guard && k < CLS_GUARD) ring[RING + k] = yv[q];
       }
     }
     if (tid < 16 * PQ)
@@ -1006,9 +1021,8 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int p = q * CLS_THREADS + tid;
-      const int64_t i = start + p;
       const uint32_t* bl = ring + ((uint32_t)(start + q * CLS_THREADS - 1) & (RING - 1)) + tid;
-      const bool coded = q < 2 * cur && p < count && (i == 0 || bl[1] != bl[0]);
+      const bool coded = q < 2 * cur && p < count && ((start == 0 && p == 0) || bl[0] != yv[q]);
       const unsigned long long bal = __ballot(coded);
       wbal[q] = bal;
       if (lane == 0 && q < 2 * cur) {
@@ -1239,8 +1253,8 @@ __device__ __forceinline__ void enc_classify_strip_body(const EncArgs& a) {
   // row y's window: linear pixels [yW + x0 - 3, yW + x1 + 3) (0 outside the
   // frame / the caller's pixel memory), loaded into registers
   uint32_t pw[STRIP_LD];
-  auto fetch_row = [&](uint32_t y) {
-    const int64_t g0 = (int64_t)y * W + x0 - 3;
+  auto fetch_row = [&](int64_t y) {   // y = -1: the window of row -1 (its end is row 0's first pixels)
+    const int64_t g0 = y * (int64_t)W + x0 - 3;
     const int64_t lo = max((int64_t)0, a.px_lo), hi = min(N, a.px_hi);
 #pragma unroll
     for (int k = 0; k < STRIP_LD; ++k) {
@@ -1249,16 +1263,19 @@ __device__ __forceinline__ void enc_classify_strip_body(const EncArgs& a) {
       pw[k] = (c < (int)(x1 - x0) + 6 && g >= lo && g < hi) ? reinterpret_cast<const uint32_t*>(fr)[g] : 0u;
     }
   };
-  auto commit_row = [&](uint32_t y) {
-    uint32_t* wr = win[y & 3];
+  auto commit_row = [&](int64_t y) {
+    uint32_t* wr = win[(uint32_t)y & 3u];
 #pragma unroll
     for (int k = 0; k < STRIP_LD; ++k) {
       const int c = tid + k * CLS_THREADS;
       if (c < (int)(x1 - x0) + 6) wr[c] = y_from_rgba(pw[k]);
     }
   };
-  // prefill rows y0-3 .. y0-1
-  for (uint32_t y = y0 >= 3 ? y0 - 3 : 0; y < y0; ++y) {
+  // prefill rows y0-3 .. y0-1, from row -1 on: the window of the row above
+  // row 0 ends with row 0's first pixels, which the last columns of row 0
+  // reference through offsets W-1 and W-3 (code.rs:141-145; round 5 width
+  // sweep: 10240 x 12 RGBA frames whose pixel W-3 only luma reference 3 predicts)
+  for (int64_t y = y0 >= 3 ? (int64_t)y0 - 3 : -1; y < (int64_t)y0; ++y) {
     fetch_row(y);
     commit_row(y);
   }

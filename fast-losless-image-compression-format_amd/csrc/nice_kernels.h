@@ -213,6 +213,8 @@ struct DecArgs {
   // tests (nice_test_set_hooks): the last strip of every frame returns at
   // once, as a block that never became resident would, so the others time out
   uint32_t test_absent_strip;
+  // dec_rows_flow: row groups per block (rows in flight)
+  uint32_t flow_k;
 };
 constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
@@ -233,6 +235,8 @@ __global__ void dec_reconstruct(DecArgs a);
 __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);
 __global__ void dec_rows8(DecArgs a);
+__global__ void dec_rows_flow(DecArgs a);   // small batches: rows in flight, LDS stamps (W <= 4096)
+constexpr uint32_t FLOW_THREADS_HOST = 512, FLOW_CTL_BYTES_HOST = 1984;   // == FLOW_THREADS, sizeof(FlowCtl)
 __global__ void dec_rows_split(DecArgs a);
 constexpr uint32_t SPLIT_THREADS_HOST = 256;   // == SPLIT_THREADS (nice_decode.hip): lanes per strip
 constexpr uint32_t SPLIT_GRAN_HOST = 8;        // == SPLIT_GRAN

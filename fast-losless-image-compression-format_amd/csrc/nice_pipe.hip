@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void pipe_checksum(const uint8_t* base, uint64
       v = *reinterpret_cast<const uint32_t*>(fr + 4 * w);
     } else {
       v = 0;
-      for (uint32_t k = 0; 4 * w + k < n; ++k) v |= (uint32_t)fr[4 * w + k] << (8 * k);
+      for (uint32_t k = 0; k < 4u && 4 * w + k < n; ++k) v |= (uint32_t)fr[4 * w + k] << (8 * k);
     }
     A += v;
     B += (unsigned long long)(w + 1) * v;
