@@ -782,8 +782,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
   unsigned long long* dstats = nullptr;
-  if (want_stats && hipMalloc(&dstats, 512) == hipSuccess) {
-    (void)hipMemsetAsync(dstats, 0, 512, st);
+  if (want_stats && hipMalloc(&dstats, 1024) == hipSuccess) {
+    (void)hipMemsetAsync(dstats, 0, 1024, st);
     a.stats = dstats;
   }
   hipLaunchKernelGGL(dec_init_entries, dim3((max_chunks + 255) / 256 < 64 ? (max_chunks + 255) / 256 : 64, n_frames),
@@ -900,14 +900,27 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   tm.end(st);
   if (dstats) {
-    unsigned long long h[64] = {0};
-    (void)hipMemcpyAsync(h, dstats, 512, hipMemcpyDeviceToHost, st);
+    unsigned long long h[128] = {0};
+    (void)hipMemcpyAsync(h, dstats, 1024, hipMemcpyDeviceToHost, st);
+    uint32_t chg[kSyncFlags] = {0};
+    (void)hipMemcpyAsync(chg, changed, 4 * kSyncFlags, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
             "[nice dec stats] rows=%llu unconverged_segs=%llu tail_unknown_segs=%llu "
             "recomputed_px=%llu fixup_rounds=%llu sync_iters=%u seg=%u nseg=%u "
             "clk[load=%llu spec=%llu fix=%llu emit=%llu]\n",
             h[0], h[1], h[2], h[3], h[4], it_count, g.seg, g.nseg, h[5], h[6], h[7], h[8]);
+    fprintf(stderr, "[nice dec stats] sync iterations that changed an entry:");
+    for (uint32_t i = 0; i < kSyncFlags; ++i) fprintf(stderr, " %u", chg[i]);
+    fprintf(stderr, " (queued %u, then settled, final)\n", queued);
+    for (int w = 0; w < 4; ++w) {   // dec_rows_flow (-DNICE_FLOW_STATS builds): cycles per row by phase
+      const unsigned long long* q = h + 64 + 8 * w;
+      if (q[7])
+        fprintf(stderr, "[nice flow stats] wave %d rows=%llu cyc/row: emit+decode=%.0f wait=%.0f ring=%.0f spec=%.0f "
+                "fix=%.0f publish=%.0f rounds/row=%.2f\n", w, q[7], (double)q[0] / q[7], (double)q[1] / q[7],
+                (double)q[2] / q[7], (double)q[3] / q[7], (double)q[4] / q[7], (double)q[5] / q[7],
+                (double)q[6] / q[7]);
+    }
     fprintf(stderr, "[nice dec stats] unknown segment tails: copies of an unknown %llu, narrowed %llu\n", h[24], h[25]);
     fprintf(stderr, "[nice dec stats] re-parse met previous parse at checkpoint:");
     for (int k = 0; k < 17; ++k) fprintf(stderr, " %d:%llu", k, h[32 + k]);

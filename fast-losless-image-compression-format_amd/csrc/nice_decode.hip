@@ -2357,7 +2357,6 @@ __device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, ui
   return true;
 }
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1); }
-
 __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   constexpr int S = ROWS_SEG;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -2411,6 +2410,13 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   };
   if (g < H) load_recs(g);
   bool ok = true;
+#ifdef NICE_FLOW_STATS   // cycle split per wave position (NICE_DEC_STATS=1): stats[64 + 8 w + k]
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define FLOW_T(k) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ts[k] += t_ - tlast; tlast = t_; }
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#else
+#define FLOW_T(k)
+#endif
   for (uint32_t y = g; y < H && ok; y += K) {
     const uint32_t s = y & (FLOW_SLOTS - 1u), sp = (y - 1u) & (FLOW_SLOTS - 1u);
     // ---- pre-pass, part 1 (no pixel values): the row's class table, each
@@ -2447,8 +2453,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         ad[p] = cur ? ZERO_IDX : ad[p];
       }
     }
+    FLOW_T(0)
     // ---- wait for the rows above
     if (y > 0 && !flow_wait(C, C.fin[sp], depmask, y)) { ok = false; break; }
+    FLOW_T(1)
     // ---- pre-pass, part 2: reference values, the row above, the entry
     uint32_t wv[S], prev[S];
 #pragma unroll
@@ -2469,6 +2477,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         r2 = ivs_exact(pr[(W - 3) + ((W - 3) >> 4)]);
       }
     }
+    FLOW_T(2)
     // ---- speculative pass
     IvS v[S];
     int lu = rows_spec<S>(v, r0, r1, r2, wv, prev);
@@ -2489,6 +2498,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       }
     };
     pub_tail();
+    FLOW_T(3)
     // ---- fix-up rounds inside the wave
     bool cur_done = !wave_cur;
     unsigned long long t0 = 0;
@@ -2523,11 +2533,13 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         for (int p = 0; p < S; ++p) asm volatile("" : "+v"(wv[p]));
         lu = rows_chain_exact<S>(v, l0, l1, l2, wv, prev, lu, go);
         if (go) {
-          if (lu >= 0) atomicCAS(&C.err, 0, NICE_E_FORMAT);   // exact inputs give exact outputs
           fin = true;
           tex = true;
         }
         pub_tail();
+#ifdef NICE_FLOW_STATS
+        ts[6] += 1;
+#endif
       } else {
         // nothing to do until the left wave's tail or the row head arrive
         if ((n & 31u) == 0u) {
@@ -2544,6 +2556,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         __builtin_amdgcn_s_sleep(1);
       }
     }
+    FLOW_T(4)
     if (!ok) break;
     if (C.err) { atomicOr(&C.abort, 1u); ok = false; break; }
     // ---- the ring row, its halos, the stamp
@@ -2555,14 +2568,18 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) pr[(W + k) + ((W + k) >> 4)] = v[k].lo;
       }
-      if (x0 + S + 2u >= W) {   // row y+1's left halo: this row's last three pixels
-        uint32_t* hh = ring + ((y + 1u) & (FLOW_SLOTS - 1u)) * RS;
-#pragma unroll
-        for (int p = 0; p < S; ++p)
-          if (p < nvalid && x0 + p + 3u >= W) hh[(int)(x0 + p - W) - 1] = v[p].lo;
-      }
+    }
+    if (wave_cur) {   // row y+1's left halo (words -4..-2): this row's columns W-3..W-1, copied
+      // from the ring words just written by the wave holding each of them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      const uint32_t col = W - 3u + lane;
+      if (lane < 3u && (col / S) / 64u == w)
+        ring[((y + 1u) & (FLOW_SLOTS - 1u)) * RS + lane - 4] = ring[s * RS + col + (col >> 4)];
     }
     if (lane == 0) flow_publish(&C.fin[s][w], y + 1u);
+    FLOW_T(5)
     // ---- off the critical path: the next row's records, the raster
     if (y + K < H) load_recs(y + K);
     if (active) {
@@ -2607,6 +2624,14 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     const int e = __hip_atomic_load(&C.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (e) set_status(&a.status[f], e);
   }
+#ifdef NICE_FLOW_STATS
+  if (lane == 0 && a.stats) {
+    // ts[7]: rows processed; k = 0 record decode, 1 wait, 2 ring reads, 3 spec, 4 fix-up, 5 ring row + stamp, 6 fix-up rounds with work
+    ts[7] = (H > g ? (H - g + K - 1) / K : 0);
+    for (int k = 0; k < 8; ++k) atomicAdd(&a.stats[64 + 8 * w + k], ts[k]);
+  }
+#endif
+#undef FLOW_T
 }
 
 // ---------------------------------------------------------------------------

@@ -939,16 +939,11 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
     const uint32_t f = ti.f;
     const int64_t start = (int64_t)ti.tt() * ENC_TILE;
     if (C == 4) {
-      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride) + start;
-      if (start + (int64_t)nti * ENC_TILE <= N) {   // block-uniform: no per-pixel bounds
+      const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)f * a.frame_stride);
 #pragma unroll
-        for (int q = 0; q < PQ; ++q) pf[q] = q < 2 * nti ? fr[q * CLS_THREADS + tid] : 0u;
-      } else {
-#pragma unroll
-        for (int q = 0; q < PQ; ++q) {
-          const int64_t j = start + q * CLS_THREADS + tid;
-          pf[q] = (q < 2 * nti && j < N) ? fr[q * CLS_THREADS + tid] : 0u;
-        }
+      for (int q = 0; q < PQ; ++q) {
+        const int64_t j = start + q * CLS_THREADS + tid;
+        pf[q] = (q < 2 * nti && j < N) ? fr[j] : 0u;
       }
     } else {   // the iteration's dwords tid, 512 + tid, 1024 + tid
       const uint8_t* fr = a.px + (uint64_t)f * a.frame_stride;
@@ -992,17 +987,13 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
       }
     }
     uint32_t yv[PQ];   // the thread's pixels in Y space (classify's X)
-    // the mirrored guard only in iterations whose ring range starts in it or
-    // wraps (block-uniform; one iteration in eight)
-    const uint32_t k0 = (uint32_t)start & (RING - 1);
-    const bool guard = k0 < (uint32_t)CLS_GUARD || k0 + (uint32_t)(cur * ENC_TILE) > (uint32_t)RING;
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       yv[q] = y_from_rgba(pxw[q]);
       if (q < 2 * cur) {
         const uint32_t k = (uint32_t)(start + q * CLS_THREADS + tid) & (RING - 1);
         ring[k] = yv[q];
-        if (guard && k < CLS_GUARD) ring[RING + k] = yv[q];
+        if (k < CLS_GUARD) ring[RING + k] = yv[q];
       }
     }
     if (tid < 16 * PQ)
