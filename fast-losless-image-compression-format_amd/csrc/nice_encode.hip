@@ -299,7 +299,7 @@ __device__ __forceinline__ uint32_t classify_fast(const TileWin& tw, int col, ui
   const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins; skipped when no lane needs it
   uint32_t lk = 11u, lt = 0u;
-  const bool need_luma = __any(!br && !sd && !l2);
+  const bool need_luma = __builtin_amdgcn_ballot_w64(!br && !sd && !l2) != 0ull;
   if (need_luma) {
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
 #pragma unroll
@@ -573,18 +573,23 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
   // three fields (an OR only adds bit 3, which 0x100 lacks; no carry: fields
   // <= 515)
   const bool sd = has_left && ((d & K3(0x3F8u)) | ((d + K3(1u)) & K3(8u))) == K3(0x100u);
-  const uint32_t sdi = (d & 7u) + 7u * ((d >> 10) & 7u) + 49u * ((d >> 20) & 7u);
-  // luma2 against the prediction (code.rs:252-292)
+  // the index f0 + 7 f1 + 49 f2 of the three 3-bit fields f (code.rs:243-245)
+  // by one 24-bit multiply: the product's bits 20..29 hold it, the partial
+  // products below stay under 2^20 (f <= 6) and the ones above start at bit 30
+  const uint32_t sdi = (__umul24(d & K3(7u), 49u | (7u << 10) | (1u << 20)) >> 20) & 0x3FFu;
+  // luma2 against the prediction (code.rs:252-292): t2 = Y(X) - Y(pred) with
+  // the test offsets, Y(pred) = pred - pg in fields 0 and 2, written as
+  // X + LUMA_KY - pred + pg (fields 17..782: no borrow or carry across fields,
+  // and only each field's value mod 256 is used below)
   const uint32_t pg = (pred >> 10) & 0xFFu;
-  const uint32_t py = (uint32_t)(__mul24((int)pg, -0x100001) + (int)(pred + K3(256u))) & K3(0xFFu);
   const uint32_t xk = X + LUMA_KY;
-  const uint32_t t2 = xk - py;
+  const uint32_t t2 = (xk - pred) + (pg | (pg << 20));
   const bool l2 = has_up && (t2 & LUMA_MASK) == 0;
   // luma against 11 references, first hit wins (code.rs:293-339)
   uint32_t lk = 11u, lt = 0u;
   // (A/B: the search made unconditional on the fast path -- more VALU per
   // pixel -- was 6 % slower at 512 frames: whole waves often skip it)
-  const bool need_luma = __any(!br && !sd && !l2);
+  const bool need_luma = __builtin_amdgcn_ballot_w64(!br && !sd && !l2) != 0ull;
   if (need_luma) {
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
     if constexpr (HEAD) {
@@ -610,7 +615,7 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
       lt = xk - rbase[ltab[m & 15u] + tid];
     }
   }
-  const uint32_t r = xr + K3(256u) - (has_left ? pred : 0u);
+  const uint32_t r = has_left ? d - K3(3u) : xr + K3(256u);   // = xr + 256 - pred per field
   // the record (nice_rec.hpp): BACK_REF and SMALL_DIFF onto the lane's
   // constant (mode range + absent slots); RGB's r, g, b fields (spread, 10-bit
   // spacing) to c0, s1, s2 by doubling g (one bit further up); LUMA2 / LUMA: g
