@@ -690,11 +690,13 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     if (sps > SPLIT_THREADS_HOST || nseg16 <= (strips - 1) * sps + 1) split = false;
   }
   const uint32_t split_frames = split ? std::min(n_frames, split_cap / strips) : 0;   // frames per launch
-  // small batches (at most one frame per CU), W <= 4096: the dataflow row
-  // kernel (rows in flight, no block barriers); NICE_DEC_FLOW=0 disables it,
-  // =k sets its row groups (default 2)
-  uint32_t flow_k = 2;
-  bool flow = !split && use_rows && !rows8 && w <= 4096 && n_frames <= (uint32_t)std::max(ctx->cus, 1);
+  // W <= 4096: the dataflow row kernel (no block barriers; dec_rows_flow).
+  // At most one frame per CU: two row groups in flight and an 8-row ring (one
+  // block per CU); larger batches: one group and a 4-row ring, so two frames
+  // share each CU.  NICE_DEC_FLOW=0 takes dec_rows, =k forces k groups (A/B).
+  uint32_t flow_k = 2, flow_ring = 8;
+  bool flow = !split && use_rows && !rows8 && w <= 4096;
+  if (n_frames > (uint32_t)std::max(ctx->cus, 1)) { flow_k = 1; flow_ring = 4; }
   if (const char* ev = getenv("NICE_DEC_FLOW")) {
     const int v = atoi(ev);
     if (v <= 0) flow = false;
@@ -702,8 +704,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   }
   const uint32_t flow_wpr = ((w + 15) / 16 + 63) / 64;
   if (flow_k * flow_wpr > FLOW_THREADS_HOST / 64) flow_k = FLOW_THREADS_HOST / 64 / flow_wpr;
-  if (flow_k + 3 > 8 || flow_k < 1) flow = false;
-  const size_t flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)8 * (w + (w >> 4) + 24) + 4) * 4;   // 8 ring rows (rows_ring_stride)
+  if (flow_k > 4 || flow_k < 1) flow = false;   // (stamps of 8 rows)
+  if (flow_k > 1) flow_ring = 8;
+  const size_t flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)flow_ring * (w + (w >> 4) + 24) + 4) * 4;   // rows_ring_stride
   if (flow_lds > 160 * 1024) flow = false;
   const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
   // the row ring in global memory: dec_rows_wide (also the split path's
@@ -882,7 +885,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows_flow, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)flow_lds));
     a.flow_k = flow_k;
-    hipLaunchKernelGGL(dec_rows_flow, dim3(n_frames), dim3(FLOW_THREADS_HOST), flow_lds, st, a);
+    a.flow_ring = flow_ring;
+    hipLaunchKernelGGL(dec_rows_flow, dim3(n_frames), dim3(64 * flow_k * flow_wpr), flow_lds, st, a);
   } else if (use_rows && rows_in_lds && rows8) {
     if (rows8_lds > 64 * 1024)
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows8, hipFuncAttributeMaxDynamicSharedMemorySize,

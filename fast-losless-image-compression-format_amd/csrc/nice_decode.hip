@@ -2306,7 +2306,8 @@ __global__ __launch_bounds__(512) void dec_rows8(DecArgs a) { dec_rows_body<512,
 // stop).
 // ---------------------------------------------------------------------------
 constexpr uint32_t FLOW_THREADS = 512;
-constexpr uint32_t FLOW_SLOTS = 8;
+constexpr uint32_t FLOW_SLOTS = 8;   // stamp slots
+
 constexpr uint32_t FLOW_MAXW = 4;
 constexpr unsigned long long FLOW_TIMEOUT = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
 struct FlowCtl {
@@ -2366,8 +2367,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   const uint32_t W = a.W, H = a.H, f = blockIdx.x;
   const uint32_t RS = rows_ring_stride(W);
   const uint32_t RB = CTL_WORDS + ROWS_RB;   // sm index of ring slot 0, pixel 0
+  const uint32_t RM = a.flow_ring - 1u;      // ring rows - 1 (4 or 8 rows)
   uint32_t* const ring = sm + RB;
-  for (uint32_t i = threadIdx.x; i < CTL_WORDS; i += FLOW_THREADS) sm[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < CTL_WORDS; i += blockDim.x) sm[i] = 0u;
   __syncthreads();
   if (a.status[f] != 0) return;   // block-uniform
   const uint32_t nseg = (W + S - 1) / S, WPR = (nseg + 63) / 64, K = a.flow_k;
@@ -2418,7 +2420,8 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
 #define FLOW_T(k)
 #endif
   for (uint32_t y = g; y < H && ok; y += K) {
-    const uint32_t s = y & (FLOW_SLOTS - 1u), sp = (y - 1u) & (FLOW_SLOTS - 1u);
+    const uint32_t s = y & (FLOW_SLOTS - 1u);                              // stamps
+    const uint32_t rs = y & RM, rsp = (y - 1u) & RM;   // ring rows
     // ---- pre-pass, part 1 (no pixel values): the row's class table, each
     // record's constant and kind bits, and the ring index of its reference
     if (lane < 16) {
@@ -2426,7 +2429,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       const unsigned long long kinds = y == 0 ? ROWS_KIND_Y0 : ROWS_KIND;
       const uint32_t rows = (CLS_ROWS_PACK >> (2 * c)) & 3u, dxp3 = (uint32_t)(CLS_PX_PACK >> (3 * c)) & 7u;
       rtab[c] = make_uint2((((uint32_t)(kinds >> (4u * c)) & 15u) << 28) | dxp3,
-                           RB + ((y - rows) & (FLOW_SLOTS - 1u)) * RS + 3u - dxp3);
+                           RB + ((y - rows) & RM) * RS + 3u - dxp3);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
@@ -2455,7 +2458,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     }
     FLOW_T(0)
     // ---- wait for the rows above
-    if (y > 0 && !flow_wait(C, C.fin[sp], depmask, y)) { ok = false; break; }
+    if (y > 0 && !flow_wait(C, C.fin[(y - 1u) & (FLOW_SLOTS - 1u)], depmask, y)) { ok = false; break; }
     FLOW_T(1)
     // ---- pre-pass, part 2: reference values, the row above, the entry
     uint32_t wv[S], prev[S];
@@ -2464,7 +2467,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       const uint32_t o = sm[ad[p]];
       wv[p] = (wk[p] & ~SP_K) | ((o + wk[p]) & SP_K);
     }
-    uint32_t* const pr = ring + sp * RS;
+    uint32_t* const pr = ring + rsp * RS;
 #pragma unroll
     for (int p = 0; p < S; ++p) prev[p] = y > 0 ? pr[lb + p] : 0u;
     IvS r0{0u, SP_K}, r1{0u, SP_K}, r2{0u, SP_K};
@@ -2561,7 +2564,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     if (C.err) { atomicOr(&C.abort, 1u); ok = false; break; }
     // ---- the ring row, its halos, the stamp
     if (active) {
-      uint32_t* rr = ring + s * RS + lb;
+      uint32_t* rr = ring + rs * RS + lb;
 #pragma unroll
       for (int p = 0; p < S; ++p) rr[p] = v[p].lo;   // padding pixels land in the row's spare words
       if (seg == 0 && y > 0) {   // row y-1's right halo: this row's first three pixels
@@ -2571,12 +2574,15 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     }
     if (wave_cur) {   // row y+1's left halo (words -4..-2): this row's columns W-3..W-1, copied
       // from the ring words just written by the wave holding each of them
+      // (a 4-row ring puts it over row y-3's left halo, which row y's first
+      // wave reads in its pre-pass: wait for that wave's first pixels)
+      if (RM < 7u && !flow_wait(C, &C.hst[s], 1u, y + 1u)) { ok = false; break; }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       const uint32_t col = W - 3u + lane;
       if (lane < 3u && (col / S) / 64u == w)
-        ring[((y + 1u) & (FLOW_SLOTS - 1u)) * RS + lane - 4] = ring[s * RS + col + (col >> 4)];
+        ring[((y + 1u) & RM) * RS + lane - 4] = ring[rs * RS + col + (col >> 4)];
     }
     if (lane == 0) flow_publish(&C.fin[s][w], y + 1u);
     FLOW_T(5)

@@ -213,8 +213,8 @@ struct DecArgs {
   // tests (nice_test_set_hooks): the last strip of every frame returns at
   // once, as a block that never became resident would, so the others time out
   uint32_t test_absent_strip;
-  // dec_rows_flow: row groups per block (rows in flight)
-  uint32_t flow_k;
+  // dec_rows_flow: row groups per block (rows in flight), ring rows (4 or 8)
+  uint32_t flow_k, flow_ring;
 };
 constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
