@@ -143,7 +143,7 @@ def max_over_ranks(value, dist, device):
 # timing phase -> the kernels that implement it (first match in the PMC summary)
 PHASE_KERNELS = {"enc_classify": ["enc_classify_pair_m", "enc_classify_pair", "enc_classify_ring", "enc_classify"],
                  "enc_tilebits": ["enc_tilebits_hist", "enc_tilebits"],
-                 "dec_reconstruct": ["dec_rows", "dec_rows_wide", "dec_reconstruct"]}
+                 "dec_reconstruct": ["dec_rows_flow", "dec_rows", "dec_rows_wide", "dec_reconstruct"]}
 
 
 def load_traffic(phase, frames, path=None):
@@ -168,7 +168,7 @@ def load_traffic(phase, frames, path=None):
 
 SQ_KERNELS = {"classify": ["nice::enc_classify_pair_m", "nice::enc_classify_pair", "nice::enc_classify_ring"],
               "pack": ["nice::enc_pack"], "sync": ["nice::dec_sync"], "emit": ["nice::dec_emit"],
-              "rundigits": ["nice::enc_rundigits"], "place": ["nice::dec_place"], "rows": ["nice::dec_rows"]}
+              "rundigits": ["nice::enc_rundigits"], "place": ["nice::dec_place"], "rows": ["nice::dec_rows_flow", "nice::dec_rows"]}
 
 
 def load_sq(px_per_run=32 * 3840 * 2160, path=None):

@@ -2358,6 +2358,46 @@ __device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, ui
   return true;
 }
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1); }
+// The speculative pass with the exact index of the last unknown pixel (-1:
+// none), for the fix-up chain's bound.  (A vote after pixel 7 switching the
+// wave to the exact step when every lane's last three pixels were exact was
+// neutral: 18.73 vs 18.64 ms at 512 frames, 10.21 vs 10.25 for one frame,
+// profiles/r05w_ab_flow_spec.log.)
+template <int S>
+__device__ __forceinline__ int rows_spec_lu(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                            const uint32_t (&prev)[S]) {
+  int lu = -1;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const IvS l1 = p >= 1 ? v[p - 1] : r0;
+    const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
+    const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
+    v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
+    lu = v[p].len ? p : lu;
+  }
+  return lu;
+}
+// Exact recompute of pixels 0..upto (lanes with upto >= 0); the second half
+// only when some lane of the wave still has unknown pixels there (one vote per
+// round: 512 x 4K reconstruct -1 %, 1024 x 1080p -2 %, profiles/r05v_ab_chunks.log;
+// votes every four pixels cost more than they saved at one frame per CU).
+template <int S>
+__device__ __forceinline__ void rows_chain_upto(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                                const uint32_t (&prev)[S], int upto) {
+  auto step = [&](int p) {
+    const uint32_t l1 = p >= 1 ? v[p - 1].lo : r0.lo;
+    const uint32_t l2 = p >= 2 ? v[p - 2].lo : (p == 1 ? r0.lo : r1.lo);
+    const uint32_t l3 = p >= 3 ? v[p - 3].lo : (p == 2 ? r0.lo : (p == 1 ? r1.lo : r2.lo));
+    const uint32_t n = rows_step_exact(l1, l2, l3, prev[p], w[p]);
+    v[p].lo = p <= upto ? n : v[p].lo;
+  };
+#pragma unroll
+  for (int p = 0; p < 8; ++p) step(p);
+  if (__ballot(upto >= 8) != 0ull) {
+#pragma unroll
+    for (int p = 8; p < 16; ++p) step(p);
+  }
+}
 __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   constexpr int S = ROWS_SEG;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -2483,7 +2523,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     FLOW_T(2)
     // ---- speculative pass
     IvS v[S];
-    int lu = rows_spec<S>(v, r0, r1, r2, wv, prev);
+    int lu = rows_spec_lu<S>(v, r0, r1, r2, wv, prev);
     bool fin = !active || lu < 0;
     bool tex = !active || lu < S - 3;
     if (w == 0 && lane == 0) {   // the row's first three pixels (lane 0: exact entry)
@@ -2534,7 +2574,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       if (__ballot(go) != 0ull) {
 #pragma unroll
         for (int p = 0; p < S; ++p) asm volatile("" : "+v"(wv[p]));
-        lu = rows_chain_exact<S>(v, l0, l1, l2, wv, prev, lu, go);
+        rows_chain_upto<S>(v, l0, l1, l2, wv, prev, go ? lu : -1);
         if (go) {
           fin = true;
           tex = true;
