@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds libnice_hip.so of a git revision into ab/NAME (for tools/abn.sh A/B runs).
-# Usage: bash tools/build_ab.sh REV NAME
+# Usage: [EXTRA="-DFOO"] bash tools/build_ab.sh REV NAME
 set -e
 REV=${1:-HEAD}; NAME=${2:-head}
 R=$(git rev-parse --show-toplevel)
@@ -8,7 +8,7 @@ T=$(mktemp -d /tmp/ab_XXXX)
 git -C "$R" archive "$REV" fast-losless-image-compression-format_amd/csrc include | tar -x -C "$T"
 cd "$T/fast-losless-image-compression-format_amd"
 for f in nice_encode nice_decode nice_capi nice_pipe nice_image; do
-  [ -f csrc/$f.hip ] && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-function \
+  [ -f csrc/$f.hip ] && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-function $EXTRA \
     -c csrc/$f.hip -o $T/$f.o &
 done
 wait
