@@ -1475,6 +1475,9 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
         bool stop = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          // rows past the slice's last event (a slice's last step is mostly
+          // empty): skipped by a uniform branch, not computed under a mask
+          if (i + 64u * k >= nev) break;
           const bool valid = i + 64u * k + lane < nev;
           const bool run = (ev[k] & EV_RUN) != 0u;
           const uint32_t incl = wave_incl_scan(c32[k]);
@@ -1486,8 +1489,10 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
         }
         if (!__any(stop)) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
+          for (int k = 0; k < 4; ++k) {
+            if (i + 64u * k >= nev) break;
             if (i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qb[k]] = r[k] | (a.rec_tag << REC_TAG_SHIFT);
+          }
           q = base;
           continue;
         }
