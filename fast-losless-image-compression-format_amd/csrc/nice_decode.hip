@@ -2362,7 +2362,12 @@ __device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, ui
   flow_acquire();
   return true;
 }
-__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1); }
+// lane l gets lane l-1's value (lane 0: 0) by a DPP wave shift: one VALU move,
+// no LDS round trip (ds_bpermute) on the hand-off path (one 4K frame 10.27 ->
+// 10.21 ms, 64 x 1080p 4.79 -> 4.74, profiles/r05zl_ab_flow_dpp.log)
+__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+}
 // The speculative pass with the exact index of the last unknown pixel (-1:
 // none), for the fix-up chain's bound.  (A vote after pixel 7 switching the
 // wave to the exact step when every lane's last three pixels were exact was
