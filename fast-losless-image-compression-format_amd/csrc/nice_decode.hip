@@ -1578,16 +1578,15 @@ __device__ __forceinline__ uint32_t unspread3(uint32_t v) {
 __device__ __forceinline__ IvS ivs_exact(uint32_t sp) { return IvS{sp, 0u}; }
 __device__ __forceinline__ IvS ivs_add(IvS a, uint32_t c) { return IvS{(a.lo + c) & SP_K, a.len}; }
 // floor((L + U) / 2) + c over an interval L: halves it unless it wraps past
-// 255, in which case the hull of both halves is [U/2, (255+U)/2].
+// 255, in which case the hull of both halves is [U/2, (255+U)/2] -- the
+// average of the whole range [0, 255], so a wrapping field is widened to that
+// before the one averaging (instead of averaging both forms and selecting).
 __device__ __forceinline__ IvS ivs_avg(IvS l, uint32_t u, uint32_t c) {
   const uint32_t s = l.lo + l.len;
   const uint32_t wm = ((s >> 8) & SP_1) * 0x3FFu;        // fields whose interval wraps
-  uint32_t lo1 = ((l.lo + u) >> 1) & SP_K;
-  uint32_t hi1 = ((s + u) >> 1) & SP_K9;
-  const uint32_t ulo = (u >> 1) & SP_K;
-  const uint32_t uhi = ((u + SP_K) >> 1) & SP_K9;
-  lo1 = (lo1 & ~wm) | (ulo & wm);
-  hi1 = (hi1 & ~wm) | (uhi & wm);
+  const uint32_t lo0 = l.lo & ~wm, s0 = (s & ~wm) | (SP_K & wm);
+  const uint32_t lo1 = ((lo0 + u) >> 1) & SP_K;
+  const uint32_t hi1 = ((s0 + u) >> 1) & SP_K9;
   return IvS{(lo1 + c) & SP_K, hi1 - lo1};
 }
 
