@@ -1814,8 +1814,11 @@ __device__ __forceinline__ uint32_t wmask(uint32_t w, int bit) {
   return (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1);   // 0 or ~0
 }
 // One pixel: kinds are selected with masks (no control flow, no SGPR masks).
+// The constant is the word itself: its kind bits (18, 28..31) only reach a
+// field's guard bits or bits >= 28 of the sums, which the masks after every
+// add clear (no carry reaches a lower field: value bits <= 255 + 255 + 512).
 __device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uint32_t wp) {
-  const uint32_t c = wp & SP_K;
+  const uint32_t c = wp;
   const IvS va = ivs_avg(l1, u, c);
   const uint32_t m1 = wmask(wp, 28), m2 = wmask(wp, 29), m3 = wmask(wp, 30);
   const uint32_t ma = wmask(wp, 31), mc = wmask(wp, 18);
@@ -1829,8 +1832,11 @@ __device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uin
 // arithmetic, no intervals.  Only after the W_CUR words are resolved.
 __device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, uint32_t l3, uint32_t u,
                                                     uint32_t wp) {
-  const uint32_t c = wp & SP_K;
-  const uint32_t va = ((((l1 + u) >> 1) & SP_K) + c) & SP_K;
+  // (l1 + u) >> 1 leaves the next field's lowest bit in each guard bit 9:
+  // with c (the word: no W_CUR bit once resolved) a field sums to <= 1022, so
+  // one mask at the end clears both
+  const uint32_t c = wp;
+  const uint32_t va = (((l1 + u) >> 1) + c) & SP_K;
   const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
   const uint32_t rlo = (sel + c) & SP_K;
   return (wp & W_AVG) ? va : rlo;
