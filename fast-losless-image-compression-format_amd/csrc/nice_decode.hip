@@ -2392,7 +2392,8 @@ __device__ __forceinline__ int rows_spec_lu(IvS (&v)[S], IvS r0, IvS r1, IvS r2,
   }
   return lu;
 }
-// Exact recompute of pixels 0..upto (lanes with upto >= 0); the second half
+// Exact recompute of pixels 0..7 and, when some lane's upto >= 8, 8..15, of
+// the lanes with upto >= 0 (their entry is exact); the second half
 // only when some lane of the wave still has unknown pixels there (one vote per
 // round: 512 x 4K reconstruct -1 %, 1024 x 1080p -2 %, profiles/r05v_ab_chunks.log;
 // votes every four pixels cost more than they saved at one frame per CU).
@@ -2404,7 +2405,13 @@ __device__ __forceinline__ void rows_chain_upto(IvS (&v)[S], IvS r0, IvS r1, IvS
     const uint32_t l2 = p >= 2 ? v[p - 2].lo : (p == 1 ? r0.lo : r1.lo);
     const uint32_t l3 = p >= 3 ? v[p - 3].lo : (p == 2 ? r0.lo : (p == 1 ? r1.lo : r2.lo));
     const uint32_t n = rows_step_exact(l1, l2, l3, prev[p], w[p]);
-    v[p].lo = p <= upto ? n : v[p].lo;
+    // a lane with an exact entry recomputes every pixel of the half (the ones
+    // past its last unknown come out equal): one select on a lane mask per
+    // pixel instead of a compare and a select (with the caller's asm pin of
+    // the words, which cost a copy of each per round, removed: 512 x 4K
+    // reconstruct 17.53 -> 16.86 ms, one 4K frame 9.56 -> 9.08,
+    // profiles/r05zq_ab_flow_chain.log)
+    v[p].lo = upto >= 0 ? n : v[p].lo;
   };
 #pragma unroll
   for (int p = 0; p < 8; ++p) step(p);
@@ -2587,8 +2594,6 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       }
       const bool go = !fin && lex && (cur_done || !curlane);
       if (__ballot(go) != 0ull) {
-#pragma unroll
-        for (int p = 0; p < S; ++p) asm volatile("" : "+v"(wv[p]));
         rows_chain_upto<S>(v, l0, l1, l2, wv, prev, go ? lu : -1);
         if (go) {
           fin = true;
