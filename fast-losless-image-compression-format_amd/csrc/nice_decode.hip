@@ -1836,10 +1836,14 @@ __device__ __forceinline__ uint32_t rows_step_exact(uint32_t l1, uint32_t l2, ui
   // with c (the word: no W_CUR bit once resolved) a field sums to <= 1022, so
   // one mask at the end clears both
   const uint32_t c = wp;
-  const uint32_t va = (((l1 + u) >> 1) + c) & SP_K;
-  const uint32_t sel = (wp & W_L1) ? l1 : (wp & (W_L1 << 1)) ? l2 : (wp & (W_L1 << 2)) ? l3 : 0u;
-  const uint32_t rlo = (sel + c) & SP_K;
-  return (wp & W_AVG) ? va : rlo;
+  // kinds as sign-extended bit masks: and / and-or / bit-insert selects, the
+  // constant added once after the average-or-copy select (instead of compare
+  // and select chains: one 4K frame reconstruct 9.02 -> 8.72 ms, 64 x 1080p
+  // 4.10 -> 3.95, profiles/r05zr_ab_flow_steps.log)
+  const uint32_t sel = (l1 & wmask(wp, 28)) | (l2 & wmask(wp, 29)) | (l3 & wmask(wp, 30));
+  const uint32_t ma = (uint32_t)((int32_t)wp >> 31);
+  const uint32_t x = (((l1 + u) >> 1) & ma) | (sel & ~ma);
+  return (x + c) & SP_K;
 }
 
 // Speculative pass over the whole segment; returns -1 when every pixel is
@@ -2373,33 +2377,38 @@ __device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, ui
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
 }
-// The speculative pass with the exact index of the last unknown pixel (-1:
-// none), for the fix-up chain's bound.  (A vote after pixel 7 switching the
-// wave to the exact step when every lane's last three pixels were exact was
-// neutral: 18.73 vs 18.64 ms at 512 frames, 10.21 vs 10.25 for one frame,
+// The speculative pass; reports which parts of the segment stayed unknown
+// (from OR trees over the interval widths instead of a compare and select per
+// pixel): any pixel, any of pixels 8..15 (the fix-up chain's second half),
+// any of the last three (the tail the next lane or wave starts from).  (A vote
+// after pixel 7 switching the wave to the exact step when every lane's last
+// three pixels were exact was neutral: 18.73 vs 18.64 ms at 512 frames,
 // profiles/r05w_ab_flow_spec.log.)
+struct SpecUnk { uint32_t any, hi, tail; };
 template <int S>
-__device__ __forceinline__ int rows_spec_lu(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
-                                            const uint32_t (&prev)[S]) {
-  int lu = -1;
+__device__ __forceinline__ SpecUnk rows_spec_unk(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
+                                                 const uint32_t (&prev)[S]) {
+  static_assert(S == 16, "halves of eight pixels");
 #pragma unroll
   for (int p = 0; p < S; ++p) {
     const IvS l1 = p >= 1 ? v[p - 1] : r0;
     const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
     const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
     v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
-    lu = v[p].len ? p : lu;
   }
-  return lu;
+  const uint32_t tail = v[13].len | v[14].len | v[15].len;
+  const uint32_t hi = tail | v[8].len | v[9].len | v[10].len | v[11].len | v[12].len;
+  const uint32_t lo = v[0].len | v[1].len | v[2].len | v[3].len | v[4].len | v[5].len | v[6].len | v[7].len;
+  return SpecUnk{lo | hi, hi, tail};
 }
-// Exact recompute of pixels 0..7 and, when some lane's upto >= 8, 8..15, of
-// the lanes with upto >= 0 (their entry is exact); the second half
+// Exact recompute of pixels 0..7 and, when some lane with `hi` goes, 8..15,
+// of the lanes with `go` (their entry is exact); the second half
 // only when some lane of the wave still has unknown pixels there (one vote per
 // round: 512 x 4K reconstruct -1 %, 1024 x 1080p -2 %, profiles/r05v_ab_chunks.log;
 // votes every four pixels cost more than they saved at one frame per CU).
 template <int S>
 __device__ __forceinline__ void rows_chain_upto(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
-                                                const uint32_t (&prev)[S], int upto) {
+                                                const uint32_t (&prev)[S], bool go, bool hi) {
   auto step = [&](int p) {
     const uint32_t l1 = p >= 1 ? v[p - 1].lo : r0.lo;
     const uint32_t l2 = p >= 2 ? v[p - 2].lo : (p == 1 ? r0.lo : r1.lo);
@@ -2411,11 +2420,11 @@ __device__ __forceinline__ void rows_chain_upto(IvS (&v)[S], IvS r0, IvS r1, IvS
     // the words, which cost a copy of each per round, removed: 512 x 4K
     // reconstruct 17.53 -> 16.86 ms, one 4K frame 9.56 -> 9.08,
     // profiles/r05zq_ab_flow_chain.log)
-    v[p].lo = upto >= 0 ? n : v[p].lo;
+    v[p].lo = go ? n : v[p].lo;
   };
 #pragma unroll
   for (int p = 0; p < 8; ++p) step(p);
-  if (__ballot(upto >= 8) != 0ull) {
+  if (__ballot(go && hi) != 0ull) {
 #pragma unroll
     for (int p = 8; p < 16; ++p) step(p);
   }
@@ -2545,9 +2554,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     FLOW_T(2)
     // ---- speculative pass
     IvS v[S];
-    int lu = rows_spec_lu<S>(v, r0, r1, r2, wv, prev);
-    bool fin = !active || lu < 0;
-    bool tex = !active || lu < S - 3;
+    const SpecUnk su = rows_spec_unk<S>(v, r0, r1, r2, wv, prev);
+    bool fin = !active || su.any == 0u;
+    bool tex = !active || su.tail == 0u;
+    const bool unk_hi = su.hi != 0u;
     if (w == 0 && lane == 0) {   // the row's first three pixels (lane 0: exact entry)
       C.head[s][0] = v[0].lo; C.head[s][1] = v[1].lo; C.head[s][2] = v[2].lo;
       flow_publish(&C.hst[s], y + 1u);
@@ -2594,7 +2604,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
       }
       const bool go = !fin && lex && (cur_done || !curlane);
       if (__ballot(go) != 0ull) {
-        rows_chain_upto<S>(v, l0, l1, l2, wv, prev, go ? lu : -1);
+        rows_chain_upto<S>(v, l0, l1, l2, wv, prev, go, unk_hi);
         if (go) {
           fin = true;
           tex = true;
