@@ -1817,13 +1817,16 @@ __device__ __forceinline__ uint32_t wmask(uint32_t w, int bit) {
 // The constant is the word itself: its kind bits (18, 28..31) only reach a
 // field's guard bits or bits >= 28 of the sums, which the masks after every
 // add clear (no carry reaches a lower field: value bits <= 255 + 255 + 512).
+// CUR = false: the caller knows no word holds W_CUR (waves without the row's
+// last columns), two instructions fewer.
+template <bool CUR = true>
 __device__ __forceinline__ IvS rows_step(IvS l1, IvS l2, IvS l3, uint32_t u, uint32_t wp) {
   const uint32_t c = wp;
   const IvS va = ivs_avg(l1, u, c);
   const uint32_t m1 = wmask(wp, 28), m2 = wmask(wp, 29), m3 = wmask(wp, 30);
-  const uint32_t ma = wmask(wp, 31), mc = wmask(wp, 18);
+  const uint32_t ma = wmask(wp, 31);
   const uint32_t slo = (l1.lo & m1) | (l2.lo & m2) | (l3.lo & m3);
-  const uint32_t slen = (l1.len & m1) | (l2.len & m2) | (l3.len & m3) | (SP_K & mc);
+  const uint32_t slen = (l1.len & m1) | (l2.len & m2) | (l3.len & m3) | (CUR ? SP_K & wmask(wp, 18) : 0u);
   const uint32_t rlo = (slo + c) & SP_K;
   return IvS{(va.lo & ma) | (rlo & ~ma), (va.len & ma) | (slen & ~ma)};
 }
@@ -2385,7 +2388,7 @@ __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
 // three pixels were exact was neutral: 18.73 vs 18.64 ms at 512 frames,
 // profiles/r05w_ab_flow_spec.log.)
 struct SpecUnk { uint32_t any, hi, tail; };
-template <int S>
+template <int S, bool CUR>
 __device__ __forceinline__ SpecUnk rows_spec_unk(IvS (&v)[S], IvS r0, IvS r1, IvS r2, const uint32_t (&w)[S],
                                                  const uint32_t (&prev)[S]) {
   static_assert(S == 16, "halves of eight pixels");
@@ -2394,7 +2397,7 @@ __device__ __forceinline__ SpecUnk rows_spec_unk(IvS (&v)[S], IvS r0, IvS r1, Iv
     const IvS l1 = p >= 1 ? v[p - 1] : r0;
     const IvS l2 = p >= 2 ? v[p - 2] : (p == 1 ? r0 : r1);
     const IvS l3 = p >= 3 ? v[p - 3] : (p == 2 ? r0 : (p == 1 ? r1 : r2));
-    v[p] = rows_step(l1, l2, l3, prev[p], w[p]);
+    v[p] = rows_step<CUR>(l1, l2, l3, prev[p], w[p]);
   }
   const uint32_t tail = v[13].len | v[14].len | v[15].len;
   const uint32_t hi = tail | v[8].len | v[9].len | v[10].len | v[11].len | v[12].len;
@@ -2554,7 +2557,10 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     FLOW_T(2)
     // ---- speculative pass
     IvS v[S];
-    const SpecUnk su = rows_spec_unk<S>(v, r0, r1, r2, wv, prev);
+    // (a wave without the row's last columns skips the W_CUR width term:
+    // 512 x 4K reconstruct -1 %, profiles/r05zt_ab_flow_curspec.log)
+    const SpecUnk su = wave_cur ? rows_spec_unk<S, true>(v, r0, r1, r2, wv, prev)
+                                : rows_spec_unk<S, false>(v, r0, r1, r2, wv, prev);
     bool fin = !active || su.any == 0u;
     bool tex = !active || su.tail == 0u;
     const bool unk_hi = su.hi != 0u;
