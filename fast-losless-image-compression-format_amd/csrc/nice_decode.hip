@@ -1572,6 +1572,13 @@ struct IvS { uint32_t lo, len; };
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {   // R | G<<8 | B<<16 -> spread
   return (v & 0xFFu) | ((v & 0xFF00u) << 2) | ((v & 0xFF0000u) << 4);
 }
+// unspread3(v) | alpha by two byte permutes of v (R), v >> 2 (G), v >> 4 (B):
+// asel = 0x0D060100 (alpha byte 0xFF) or 0x0C060100 (0x00); 4 instructions
+// per pixel instead of 7
+__device__ __forceinline__ uint32_t unspread3_perm(uint32_t v, uint32_t asel) {
+  const uint32_t rg = __builtin_amdgcn_perm(v >> 2, v, 0x0C0C0500u);
+  return __builtin_amdgcn_perm(v >> 4, rg, asel);
+}
 __device__ __forceinline__ uint32_t unspread3(uint32_t v) {
   return (v & 0xFFu) | ((v >> 2) & 0xFF00u) | ((v >> 4) & 0xFF0000u);
 }
@@ -2000,6 +2007,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
   uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
   const uint32_t OC = a.out_channels;
   const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const uint32_t asel = alpha ? 0x0D060100u : 0x0C060100u;   // unspread3_perm
   const bool vec_rec = (W & 3u) == 0 && nvalid == S;
   const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) ||
                        (OC == 3 && S % 16 == 0 && (W & 15u) == 0 && nvalid == S);
@@ -2234,18 +2242,18 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
 #pragma unroll
         for (int q = 0; q < S / 4; ++q)
-          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
-                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+          o[q] = make_uint4(unspread3_perm(v[4 * q].lo, asel), unspread3_perm(v[4 * q + 1].lo, asel),
+                            unspread3_perm(v[4 * q + 2].lo, asel), unspread3_perm(v[4 * q + 3].lo, asel));
       } else if (vec_out) {
         if constexpr (S % 16 == 0) {
           uint32_t b[3 * S / 4];
 #pragma unroll
           for (int q = 0; q < S / 4; ++q) {
-            const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
-            const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
-            b[3 * q] = u0 | (u1 << 24);
-            b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
-            b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+            const uint32_t u0 = unspread3_perm(v[4 * q].lo, 0x0C060100u), u1 = unspread3_perm(v[4 * q + 1].lo, 0x0C060100u);
+            const uint32_t u2 = unspread3_perm(v[4 * q + 2].lo, 0x0C060100u), u3 = unspread3_perm(v[4 * q + 3].lo, 0x0C060100u);
+            b[3 * q] = __builtin_amdgcn_perm(u1, u0, 0x04020100u);       // R0 G0 B0 R1
+            b[3 * q + 1] = __builtin_amdgcn_perm(u2, u1, 0x05040201u);   // G1 B1 R2 G2
+            b[3 * q + 2] = __builtin_amdgcn_perm(u3, u2, 0x06050402u);   // B2 R3 G3 B3
           }
           uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
 #pragma unroll
@@ -2458,6 +2466,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
   const uint32_t OC = a.out_channels;
   const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const uint32_t asel = alpha ? 0x0D060100u : 0x0C060100u;   // unspread3_perm
   const bool vec_rec = (W & 3u) == 0 && nvalid == S;
   const bool vec_out = (OC == 4 && (W & 3u) == 0 && nvalid == S) ||
                        (OC == 3 && (W & 15u) == 0 && nvalid == S);
@@ -2670,17 +2679,17 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
 #pragma unroll
         for (int q = 0; q < S / 4; ++q)
-          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
-                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+          o[q] = make_uint4(unspread3_perm(v[4 * q].lo, asel), unspread3_perm(v[4 * q + 1].lo, asel),
+                            unspread3_perm(v[4 * q + 2].lo, asel), unspread3_perm(v[4 * q + 3].lo, asel));
       } else if (vec_out) {
         uint32_t b[3 * S / 4];
 #pragma unroll
         for (int q = 0; q < S / 4; ++q) {
-          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
-          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
-          b[3 * q] = u0 | (u1 << 24);
-          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
-          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+          const uint32_t u0 = unspread3_perm(v[4 * q].lo, 0x0C060100u), u1 = unspread3_perm(v[4 * q + 1].lo, 0x0C060100u);
+          const uint32_t u2 = unspread3_perm(v[4 * q + 2].lo, 0x0C060100u), u3 = unspread3_perm(v[4 * q + 3].lo, 0x0C060100u);
+          b[3 * q] = __builtin_amdgcn_perm(u1, u0, 0x04020100u);       // R0 G0 B0 R1
+          b[3 * q + 1] = __builtin_amdgcn_perm(u2, u1, 0x05040201u);   // G1 B1 R2 G2
+          b[3 * q + 2] = __builtin_amdgcn_perm(u3, u2, 0x06050402u);   // B2 R3 G3 B3
         }
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
 #pragma unroll
@@ -2875,6 +2884,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
   uint8_t* outp = a.px_out + (uint64_t)f * a.px_stride;
   const uint32_t OC = a.out_channels;
   const uint32_t alpha = (a.flags & NICE_DEC_ALPHA_FILL_FF) ? 0xFF000000u : 0u;
+  const uint32_t asel = alpha ? 0x0D060100u : 0x0C060100u;   // unspread3_perm
   const bool vec_rec = ((W | c0) & 3u) == 0 && nvalid == S;
   const bool vec_out = (OC == 4 && ((W | c0) & 3u) == 0 && nvalid == S) ||
                        (OC == 3 && ((W | c0) & 15u) == 0 && nvalid == S);
@@ -3121,17 +3131,17 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 4);
 #pragma unroll
         for (int q = 0; q < S / 4; ++q)
-          o[q] = make_uint4(unspread3(v[4 * q].lo) | alpha, unspread3(v[4 * q + 1].lo) | alpha,
-                            unspread3(v[4 * q + 2].lo) | alpha, unspread3(v[4 * q + 3].lo) | alpha);
+          o[q] = make_uint4(unspread3_perm(v[4 * q].lo, asel), unspread3_perm(v[4 * q + 1].lo, asel),
+                            unspread3_perm(v[4 * q + 2].lo, asel), unspread3_perm(v[4 * q + 3].lo, asel));
       } else if (vec_out) {
         uint32_t b[3 * S / 4];
 #pragma unroll
         for (int q = 0; q < S / 4; ++q) {
-          const uint32_t u0 = unspread3(v[4 * q].lo), u1 = unspread3(v[4 * q + 1].lo);
-          const uint32_t u2 = unspread3(v[4 * q + 2].lo), u3 = unspread3(v[4 * q + 3].lo);
-          b[3 * q] = u0 | (u1 << 24);
-          b[3 * q + 1] = (u1 >> 8) | (u2 << 16);
-          b[3 * q + 2] = (u2 >> 16) | (u3 << 8);
+          const uint32_t u0 = unspread3_perm(v[4 * q].lo, 0x0C060100u), u1 = unspread3_perm(v[4 * q + 1].lo, 0x0C060100u);
+          const uint32_t u2 = unspread3_perm(v[4 * q + 2].lo, 0x0C060100u), u3 = unspread3_perm(v[4 * q + 3].lo, 0x0C060100u);
+          b[3 * q] = __builtin_amdgcn_perm(u1, u0, 0x04020100u);       // R0 G0 B0 R1
+          b[3 * q + 1] = __builtin_amdgcn_perm(u2, u1, 0x05040201u);   // G1 B1 R2 G2
+          b[3 * q + 2] = __builtin_amdgcn_perm(u3, u2, 0x06050402u);   // B2 R3 G3 B3
         }
         uint4* o = reinterpret_cast<uint4*>(outp + pix * 3);
 #pragma unroll
