@@ -1445,16 +1445,22 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
   bool err = false;
   // 256 events per step: 4 rows of 64 consecutive events (coalesced loads and
   // record stores), prefix sums per row plus the rows before
-  uint32_t nx[4];   // the next step's events, loaded one step ahead
+  // the next step's events, loaded one step ahead and unconditionally (lanes
+  // past the slice's last event read that event again and are masked where
+  // used): with every load issued, the compiler's wait at the top of a step
+  // leaves the next step's four in flight (a conditional load with a zero
+  // fill made it wait for all of them)
+  if (i_first >= nev) return;
+  const uint32_t ev_last = nev - 1u;
+  uint32_t nx[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) nx[k] = i_first + 64u * k + lane < nev ? evp[ev_word(i_first + 64u * k + lane)] : 0u;
+  for (int k = 0; k < 4; ++k) nx[k] = evp[ev_word(min(i_first + 64u * k + lane, ev_last))];
   for (uint32_t i = i_first; i < nev; i += 256u) {
     uint32_t ev[4], r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       ev[k] = nx[k];
-      const uint32_t y = i + 256u + 64u * k + lane;
-      nx[k] = y < nev ? evp[ev_word(y)] : 0u;
+      nx[k] = evp[ev_word(min(i + 256u + 64u * k + lane, ev_last))];
     }
     // fast path (nearly every step): every count < 2^16, so positions and
     // sums stay 32-bit (q <= N <= 2^30), and no event reaches the frame end or
