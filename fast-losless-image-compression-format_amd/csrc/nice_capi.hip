@@ -482,8 +482,16 @@ struct DecLayout {
 // previous one changed nothing), then the device-side settle (dec_sync_settle)
 // and one more iteration behind its flag: no host round trip.  Flags: the
 // queued iterations', the settle's, the last iteration's.
-constexpr uint32_t kSyncQueued = 8, kSyncFlags = kSyncQueued + 2;
-constexpr uint32_t kSettledFlag = kSyncQueued, kFinalFlag = kSyncQueued + 1;
+constexpr uint32_t kSyncQueuedMax = 16, kSyncFlags = kSyncQueuedMax + 2;
+constexpr uint32_t kSettledFlag = kSyncQueuedMax, kFinalFlag = kSyncQueuedMax + 1;
+// 16: a single 4K SYN-v1 frame needs 5 (with 4 it falls to the serial
+// settle: 3.3 s); each early-exiting launch past the fixpoint costs ~5 us
+// (one 4K frame: resync 0.29 -> 0.34 ms for 8 -> 16, profiles/r05zq3_ab_syncq.log)
+#ifndef NICE_SYNC_QUEUED
+#define NICE_SYNC_QUEUED 16
+#endif
+constexpr uint32_t kSyncQueued = NICE_SYNC_QUEUED;
+static_assert(kSyncQueued >= 1 && kSyncQueued <= kSyncQueuedMax, "queued sync iterations");
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf,
                      uint32_t ev_cap, uint32_t subs, size_t hand = 0) {
   DecLayout L{};
@@ -800,7 +808,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   uint32_t queued = std::min(kSyncQueued, max_chunks + 1);
   if (const char* ev = getenv("NICE_DEC_SYNC_QUEUED")) {   // tests: fewer queued iterations
     const uint32_t v = (uint32_t)atoi(ev);
-    if (v >= 1 && v < queued) queued = v;
+    if (v >= 1 && v <= kSyncQueuedMax) queued = std::min(v, max_chunks + 1);
   }
   uint32_t* fchanged = (uint32_t*)(base + L.o_fchanged);
   NICE_HIP(hipMemsetAsync(changed, 0, 4 * kSyncFlags, st));
