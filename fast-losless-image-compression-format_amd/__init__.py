@@ -284,7 +284,10 @@ def decode_batch(streams, stream_len, width: int, height: int, out_channels: int
     if host_len is None:
         rc = lib().nice_decode_batch_dev(*args, *tail)
     else:
-        hl = (ctypes.c_uint64 * n)(*[int(x) for x in host_len])
+        hl_list = [int(x) for x in host_len]
+        if len(hl_list) != n:   # a short list would be zero padded: lengths the device does not hold
+            raise NiceError(E_ARG, f"host_len has {len(hl_list)} entries for {n} frames")
+        hl = (ctypes.c_uint64 * n)(*hl_list)
         rc = lib().nice_decode_batch_dev_hl(*args, ctypes.cast(hl, ctypes.c_void_p), *tail)
     _check(rc, "nice_decode_batch_dev")
 
@@ -346,6 +349,7 @@ class Pipeline:
 
     def _sums(self, n, enc):
         if not getattr(self, "_ck", False):
+            lib().nice_pipe_set_checksums(self.ptr, None, None)
             return None
         buf = (ctypes.c_uint64 * max(n, 1))()
         _check(lib().nice_pipe_set_checksums(self.ptr, buf if enc else None, None if enc else buf),
@@ -367,9 +371,11 @@ class Pipeline:
         caps = [o.numel() if hasattr(o, "numel") else len(o) for o in outs]
         lens = (ctypes.c_uint64 * max(n, 1))()
         co = self.channels if channels_out is None else channels_out
-        _check(lib().nice_pipe_encode(self.ptr, src, n, co, dst, min(caps) if caps else 0, lens),
-               "nice_pipe_encode")
-        self._sums_done(sums, n)
+        try:
+            rc = lib().nice_pipe_encode(self.ptr, src, n, co, dst, min(caps) if caps else 0, lens)
+        finally:   # the pipe must not keep pointing at `sums` once it is freed
+            self._sums_done(sums, n)
+        _check(rc, "nice_pipe_encode")
         return [int(lens[i]) for i in range(n)]
 
     def decode(self, streams, lengths, outs, out_channels: int | None = None,
@@ -384,8 +390,10 @@ class Pipeline:
         ln = (ctypes.c_uint64 * max(n, 1))(*lengths)
         status = (ctypes.c_int32 * max(n, 1))()
         oc = self.channels if out_channels is None else out_channels
-        rc = lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status)
-        self._sums_done(sums, n)
+        try:
+            rc = lib().nice_pipe_decode(self.ptr, src, ln, n, oc, dst, flags, status)
+        finally:
+            self._sums_done(sums, n)
         st = [int(status[i]) for i in range(n)]
         if rc != 0 and (raise_on_error or rc not in st):
             _check(rc, "nice_pipe_decode")

@@ -6,11 +6,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <algorithm>
 #include <vector>
 
 #include "../../include/nice.h"
+#include "../../include/nice_test.h"
 #include "nice_format.h"
 #include "nice_bits.hpp"
 #include "nice_kernels.h"
@@ -49,6 +51,13 @@ struct Arena {
 };
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Test / A/B options (include/nice_test.h; nice_test_set_option): stored as
+// value + 1, 0 = unset.  Nothing in the library reads the environment.
+std::atomic<int64_t> g_opt[NICE_OPT_COUNT];
+inline bool opt_set(int id) { return g_opt[id].load(std::memory_order_relaxed) != 0; }
+inline int64_t opt_val(int id) { return g_opt[id].load(std::memory_order_relaxed) - 1; }
+inline bool opt_on(int id) { return opt_set(id) && opt_val(id) != 0; }
 
 // Encoder scratch layout. The zero-per-launch block comes first (memset once).
 struct EncLayout {
@@ -317,8 +326,8 @@ static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, u
 enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR, CLS_K_TWIN };
 static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
   if (w < 3) return CLS_K_TINY;
-  if (!aligned || getenv("NICE_ENC_NO_RING")) return CLS_K_WINDOW;
-  static const bool no_pair = getenv("NICE_ENC_NO_PAIR") != nullptr;   // A/B: one tile per iteration
+  if (!aligned || opt_on(NICE_OPT_ENC_NO_RING)) return CLS_K_WINDOW;
+  const bool no_pair = opt_on(NICE_OPT_ENC_NO_PAIR);   // A/B: one tile per iteration
   if (channels == 4 && w <= CLS_PAIR_MAX_W && !no_pair) return CLS_K_PAIR;
   if (w <= CLS_RING_MAX_W) return CLS_K_RING;
   if (channels == 4 && w % ENC_TILE == 0) return CLS_K_STRIP;
@@ -493,7 +502,7 @@ constexpr uint32_t kSettledFlag = kSyncQueuedMax, kFinalFlag = kSyncQueuedMax + 
 constexpr uint32_t kSyncQueued = NICE_SYNC_QUEUED;
 static_assert(kSyncQueued >= 1 && kSyncQueued <= kSyncQueuedMax, "queued sync iterations");
 DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint64_t npx, size_t rowbuf,
-                     uint32_t ev_cap, uint32_t subs, size_t hand = 0) {
+                     uint32_t ev_cap, uint32_t subs, size_t hand = 0, bool abort_flags = false) {
   DecLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes, 256); return r; };
@@ -516,7 +525,7 @@ DecLayout dec_layout(uint32_t n_frames, uint32_t max_chunks, uint32_t n_ck, uint
   L.o_items = take(ev_cap ? (size_t)n_frames * max_chunks * subs * 4 : 0);
   L.o_icount = take(ev_cap ? (size_t)n_frames * 4 : 0);
   L.o_hand = take(hand);
-  L.o_abort = take(hand ? (size_t)n_frames * 4 : 0);
+  L.o_abort = take(hand || abort_flags ? (size_t)n_frames * 4 : 0);
   L.total = o;
   return L;
 }
@@ -651,8 +660,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   for (uint64_t l : lens) total_bits += l * 8 > D ? l * 8 - D : 0;
   uint32_t cb = DEC_MIN_CHUNK_BITS;
   while (cb < DEC_MAX_CHUNK_BITS && total_bits / (2ull * cb) > 256ull * 8 * 64 * 2) cb *= 2;
-  if (const char* ev = getenv("NICE_DEC_SLICE_BITS")) {   // tests: force a slice size
-    const uint32_t v = (uint32_t)atoi(ev);
+  if (opt_set(NICE_OPT_DEC_SLICE_BITS)) {   // tests: force a slice size
+    const uint32_t v = (uint32_t)opt_val(NICE_OPT_DEC_SLICE_BITS);
     if (v >= DEC_MIN_CHUNK_BITS && v <= DEC_MAX_CHUNK_BITS && (v & (v - 1)) == 0) cb = v;
   }
   const uint32_t max_chunks = max_len * 8 > D ? (uint32_t)((max_len * 8 - D + cb - 1) / cb) : 1;
@@ -661,7 +670,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // multi-wave row kernel for 64 <= W <= 16384 (one lane per 16-pixel segment),
   // single-wave kernel otherwise
   const uint32_t rows_thr = ((w + 15) / 16 + 63) / 64 * 64;
-  const bool single_wave = getenv("NICE_DEC_SINGLE_WAVE") != nullptr;
+  const bool single_wave = opt_on(NICE_OPT_DEC_SINGLE_WAVE);
   const bool use_rows = w >= 64 && rows_thr <= 1024 && !single_wave;
   const size_t rows_lds = ((size_t)rows_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;   // rows_ring_stride
   const bool rows_in_lds = rows_thr <= 512 && rows_lds + 1024 <= 160 * 1024;   // + static LDS
@@ -675,7 +684,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const uint32_t rows8_thr = ((w + 7) / 8 + 63) / 64 * 64;
   const size_t rows8_lds = ((size_t)rows8_thr * 7 + 8 + (size_t)4 * (w + (w >> 4) + 24)) * 4;
   bool rows8 = false;
-  if (const char* ev = getenv("NICE_DEC_SEG")) rows8 = atoi(ev) == 8 && use_rows && rows_in_lds &&
+  if (opt_set(NICE_OPT_DEC_SEG)) rows8 = opt_val(NICE_OPT_DEC_SEG) == 8 && use_rows && rows_in_lds &&
                                                        rows8_thr <= 512 && rows8_lds <= 160 * 1024;
   // wide frames, few of them: strips of <= 256 segments on separate CUs
   // (dec_rows_split; its blocks wait on each other, so they should all be
@@ -687,7 +696,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const uint32_t nseg16 = (w + 15) / 16;
   const uint32_t split_cap = (uint32_t)std::max(ctx->cus / 2, 1);
   uint32_t strips = (nseg16 + SPLIT_THREADS_HOST - 1) / SPLIT_THREADS_HOST;
-  if (const char* ev = getenv("NICE_DEC_SPLIT")) strips = (uint32_t)atoi(ev);
+  if (opt_set(NICE_OPT_DEC_SPLIT)) strips = (uint32_t)opt_val(NICE_OPT_DEC_SPLIT);
   // <= 16384 columns: only when the whole batch fits at once (else one block
   // per frame is the better use of the CUs); wider: always, in frame chunks
   bool split = !single_wave && w >= 64 && strips >= 2 && strips <= split_cap &&
@@ -705,8 +714,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   uint32_t flow_k = 2, flow_ring = 8;
   bool flow = !split && use_rows && !rows8 && w <= 4096;
   if (n_frames > (uint32_t)std::max(ctx->cus, 1)) { flow_k = 1; flow_ring = 4; }
-  if (const char* ev = getenv("NICE_DEC_FLOW")) {
-    const int v = atoi(ev);
+  if (opt_set(NICE_OPT_DEC_FLOW)) {
+    const int v = (int)opt_val(NICE_OPT_DEC_FLOW);
     if (v <= 0) flow = false;
     else flow_k = (uint32_t)v;
   }
@@ -717,6 +726,9 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   const size_t flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)flow_ring * (w + (w >> 4) + 24) + 4) * 4;   // rows_ring_stride
   if (flow_lds > 160 * 1024) flow = false;
   const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
+  // per-frame redo flags: the split kernel's, and the dataflow kernel's (a
+  // wait that timed out sends the frame to the barrier kernel)
+  const bool want_abort = split || flow;
   // the row ring in global memory: dec_rows_wide (also the split path's
   // fallback) or dec_reconstruct without room in LDS
   const size_t ring_rows = use_rows ? (size_t)n_frames * 4 * (w + (w >> 4) + 24) * 4
@@ -725,18 +737,18 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // keep the first sync pass's pixel events (one per >= 4 bits of a slice;
   // a slice with more parses its events again in dec_emit) unless the scratch
   // does not fit, then every slice is parsed again in dec_emit
-  uint32_t ev_cap = getenv("NICE_DEC_NO_EVENTS") ? 0u : cb / 4;
-  if (const char* ev = getenv("NICE_DEC_EV_CAP")) {   // tests: force event overflow
-    const uint32_t v = (uint32_t)atoi(ev);
+  uint32_t ev_cap = opt_on(NICE_OPT_DEC_NO_EVENTS) ? 0u : cb / 4;
+  if (opt_set(NICE_OPT_DEC_EV_CAP)) {   // tests: force event overflow
+    const uint32_t v = (uint32_t)opt_val(NICE_OPT_DEC_EV_CAP);
     if (ev_cap && v >= 4 && v % 4 == 0 && v < ev_cap) ev_cap = v;
   }
   const uint32_t subs = cb / DEC_EMIT_BITS;
-  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, ev_cap, subs, hand);
+  DecLayout L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, ev_cap, subs, hand, want_abort);
   int rc = ctx->dec.grow(L.total);
   if (rc && ev_cap) {
     (void)hipGetLastError();   // the failed allocation
     ev_cap = 0;
-    L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, 0, subs, hand);
+    L = dec_layout(n_frames, max_chunks, n_ck, N, rowbuf, 0, subs, hand, want_abort);
     rc = ctx->dec.grow(L.total);
   }
   if (rc) return rc;
@@ -770,7 +782,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   a.seg = g.seg;
   a.nseg = g.nseg;
   a.rows_in_lds = g.in_lds ? 1u : 0u;
-  a.parse_slow = getenv("NICE_DEC_SLOW_PARSE") ? 1u : 0u;   // tests / A/B: the general parse only
+  a.parse_slow = opt_on(NICE_OPT_DEC_SLOW_PARSE) ? 1u : 0u;   // tests / A/B: the general parse only
   a.rowbuf = (uint32_t*)(base + L.o_rowbuf);
   uint32_t* changed = (uint32_t*)(base + L.o_changed);
   if (ev_cap) {
@@ -791,7 +803,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     NICE_HIP(hipGetLastError());
     return NICE_OK;
   }
-  static const bool want_stats = getenv("NICE_DEC_STATS") != nullptr;
+  const bool want_stats = opt_on(NICE_OPT_DEC_STATS);
   unsigned long long* dstats = nullptr;
   if (want_stats && hipMalloc(&dstats, 1024) == hipSuccess) {
     (void)hipMemsetAsync(dstats, 0, 1024, st);
@@ -806,8 +818,8 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // one, and one more iteration for the slices the settle moved
   uint32_t it_count = 0;
   uint32_t queued = std::min(kSyncQueued, max_chunks + 1);
-  if (const char* ev = getenv("NICE_DEC_SYNC_QUEUED")) {   // tests: fewer queued iterations
-    const uint32_t v = (uint32_t)atoi(ev);
+  if (opt_set(NICE_OPT_DEC_SYNC_QUEUED)) {   // tests: fewer queued iterations
+    const uint32_t v = (uint32_t)opt_val(NICE_OPT_DEC_SYNC_QUEUED);
     if (v >= 1 && v <= kSyncQueuedMax) queued = std::min(v, max_chunks + 1);
   }
   uint32_t* fchanged = (uint32_t*)(base + L.o_fchanged);
@@ -820,14 +832,20 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     tm.end(st);
   }
   tm.begin(NICE_PH_DEC_RESYNC, st);
-  hipLaunchKernelGGL(dec_sync_settle, dim3(n_frames), dim3(64), 0, st, a, changed + queued - 1, fchanged,
+  hipLaunchKernelGGL(dec_sync_settle, dim3(n_frames), dim3(512), 0, st, a, changed + queued - 1, fchanged,
                      changed + kSettledFlag);
+  // the last iteration, for the slices the settle moved: it must change no
+  // entry; a frame where it does (a settle that disagreed with dec_sync) is
+  // failed by dec_scan instead of decoded from a non-fixpoint
+  NICE_HIP(hipMemsetAsync(fchanged, 0, (size_t)n_frames * 4, st));
   hipLaunchKernelGGL(dec_sync, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a, changed + kFinalFlag,
-                     changed + kSettledFlag, nullptr);
+                     changed + kSettledFlag, fchanged);
   tm.end(st);
   // the last sync iteration (no entry changed) already produced chunk_px
   tm.begin(NICE_PH_DEC_SCAN, st);
+  a.unsettled = fchanged;
   hipLaunchKernelGGL(dec_scan, dim3(n_frames), dim3(1024), 0, st, a);
+  a.unsettled = nullptr;
   // strict: the reads where the reference's refill loop would wrap (frames
   // whose tables are all <= 25 bits return at once)
   if (flags & NICE_DEC_STRICT_REFERENCE) hipLaunchKernelGGL(dec_strict_refill, cgrid, dim3(DEC_PARSE_THREADS), 0, st, a);
@@ -839,7 +857,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     // region moved or resized (other data may have held it) or the tags wrap.
     const uint64_t words = (uint64_t)n_frames * a.rec_stride;
     if (a.recs != ctx->rec_region || words != ctx->rec_words || ctx->dec.gen != ctx->rec_gen ||
-        ctx->rec_epoch >= 15u || getenv("NICE_DEC_REC_CLEAR")) {
+        ctx->rec_epoch >= 15u || opt_on(NICE_OPT_DEC_REC_CLEAR)) {
       NICE_HIP(hipMemsetAsync(a.recs, 0, words * 4, st));
       ctx->rec_region = a.recs;
       ctx->rec_words = words;
@@ -894,7 +912,26 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
                                    (int)flow_lds));
     a.flow_k = flow_k;
     a.flow_ring = flow_ring;
+    a.hand_abort = (uint32_t*)(base + L.o_abort);
+    NICE_HIP(hipMemsetAsync(a.hand_abort, 0, (size_t)n_frames * 4, st));
+    a.test_absent_strip = opt_on(NICE_OPT_TEST_FLOW_ABSENT) ? 1u : 0u;
     hipLaunchKernelGGL(dec_rows_flow, dim3(n_frames), dim3(64 * flow_k * flow_wpr), flow_lds, st, a);
+    a.test_absent_strip = 0;
+    // fallback: frames whose waits timed out (the workgroup was
+    // preempted or time-sliced past the bound) go to the barrier kernel; its
+    // blocks return at once for every other frame
+    DecArgs r = a;
+    r.redo = 1;
+    if (rows_in_lds) {
+      if (rows_lds > 64 * 1024)
+        NICE_HIP(hipFuncSetAttribute((const void*)dec_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)rows_lds));
+      hipLaunchKernelGGL(dec_rows, dim3(n_frames), dim3(rows_thr), rows_lds, st, r);
+    } else {
+      hipLaunchKernelGGL(dec_rows_wide, dim3(n_frames), dim3(rows_thr), ((size_t)rows_thr * 7 + 8) * 4, st, r);
+    }
+    ctx->split_abort = a.hand_abort;
+    ctx->split_frames = n_frames;
   } else if (use_rows && rows_in_lds && rows8) {
     if (rows8_lds > 64 * 1024)
       NICE_HIP(hipFuncSetAttribute((const void*)dec_rows8, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1316,6 +1353,16 @@ int nice_test_split_redos(nice_ctx* ctx, uint32_t* split_frames, uint32_t* redos
   NICE_HIP(hipMemcpy(h.data(), ctx->split_abort, h.size() * 4, hipMemcpyDeviceToHost));
   for (uint32_t v : h) *redos += v == SPLIT_REDO ? 1u : 0u;
   return NICE_OK;
+}
+
+int nice_test_set_option(int id, int64_t value) {
+  if (id < 0 || id >= NICE_OPT_COUNT) return NICE_E_ARG;
+  g_opt[id].store(value < 0 ? 0 : value + 1, std::memory_order_relaxed);
+  return NICE_OK;
+}
+
+void nice_test_reset_options(void) {
+  for (auto& o : g_opt) o.store(0, std::memory_order_relaxed);
 }
 
 const char* nice_phase_name(int phase) {

@@ -41,6 +41,12 @@ __device__ __forceinline__ void set_status(int32_t* st, int32_t code) {
   atomicCAS(reinterpret_cast<int*>(st), 0, code);
 }
 
+// chunk geometry: chunk j of frame f covers bits [D + j*CB, D + (j+1)*CB)
+__device__ __forceinline__ uint32_t n_chunks(uint64_t len, uint64_t D, uint32_t cb) {
+  const uint64_t bits = len * 8;
+  return bits > D ? (uint32_t)((bits - D + cb - 1) / cb) : 0u;
+}
+
 // ---------------------------------------------------------------------------
 // D0: tables. One block of 256 threads per frame.
 // ---------------------------------------------------------------------------
@@ -65,6 +71,14 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
   const uint32_t h = ((uint32_t)s[8] << 24) | ((uint32_t)s[9] << 16) | ((uint32_t)s[10] << 8) | s[11];
   const uint32_t ch = s[12];
   if (w != a.W || h != a.H) {
+    if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_ARG);
+    return;
+  }
+  // the host sized the slice scratch from its copy of the lengths
+  // (nice_decode_batch_dev_hl): a device length past that bound or the stream
+  // stride fails the frame before any kernel indexes slices by it
+  if (len > a.stream_stride ||
+      n_chunks(len, FILE_HEADER_BYTES * 8 + TABLE_HEADER_BITS, a.chunk_bits) > a.max_chunks) {
     if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_ARG);
     return;
   }
@@ -595,11 +609,6 @@ __device__ __forceinline__ unsigned long long ps_pack(unsigned long long rel, ui
   return rel | ((unsigned long long)dk << 44);
 }
 
-// chunk geometry: chunk j of frame f covers bits [D + j*CB, D + (j+1)*CB)
-__device__ __forceinline__ uint32_t n_chunks(uint64_t len, uint64_t D, uint32_t cb) {
-  const uint64_t bits = len * 8;
-  return bits > D ? (uint32_t)((bits - D + cb - 1) / cb) : 0u;
-}
 
 // Initial entry guesses: every slice starts at its first bit, at a prefix.
 __global__ __launch_bounds__(256) void dec_init_entries(DecArgs a) {
@@ -807,60 +816,139 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// D1b: the fixpoint on the device.  After the queued Jacobi iterations, a frame
-// whose entries still changed in the last one (fchanged) gets them by one
-// sequential parse: lane 0 of the frame's wave walks its slices in order, each
-// from the previous slice's exit, with the same stop rule as dec_sync (slice
-// end, stream end + 64 bits, more pixels than the frame), and writes every
-// entry.  A dec_sync launch after this one (prev = *settled) re-parses the
-// slices whose entries moved, which brings their pixel counts, checkpoints and
-// meeting points up to date; its exits then equal the entries.  Self-
-// synchronisation settles ordinary streams within two or three iterations, so
-// this is a bound on pathological ones, not a path streams normally take --
-// and it replaces the host's fixpoint check, so the call never waits.
+// D1b: the fixpoint on the device, for frames whose entries still changed in the
+// last queued Jacobi iteration (fchanged).  The exact entries are the serial
+// chain E_0 = 0, E_{j+1} = exit(j, E_j) (code.rs:573-684 is one parse); what
+// the Jacobi iterations left is used as far as it is provably on that chain:
+//  * slice j is consistent when it was last parsed from its current entry
+//    (last[j] == entry[j]): then entry[j+1] is exit(j, entry[j]);
+//  * so a walk that arrives at slice j with the exact entry x == entry[j] of a
+//    consistent slice continues at entry[j+1] without parsing, and only the
+//    slices whose entry or parse is stale are parsed.
+// The frame's slices are cut into contiguous ranges, one per lane of the
+// block (512 lanes).  Round 0: every lane walks its range from the entry its
+// first slice holds, skipping consistent slices, parsing the others and
+// writing their exits as the next entries; the first range starts exact
+// (E_0 = 0).  A round leaves each range internally consistent.  Then a lane
+// whose start differs from its left neighbour's exit walks again from that
+// exit, parsing only until it meets an entry it already holds (from there its
+// range is consistent, so its exit stands); rounds repeat until no start
+// changes.  Range r is exact once ranges 0..r-1 are, so this terminates; with
+// self-synchronisation within a range it ends after round 1, and a stream
+// that never re-synchronises costs one serial parse of its dirty slices, as
+// the reference's own decode does.  (Round 5's settle had one lane walk every
+// slice from slice 0: 3.3 s for a 4K frame that missed the fixpoint by one
+// queued iteration.)  A dec_sync launch after this one (prev = *settled)
+// re-parses the slices whose entries moved, bringing their pixel counts,
+// checkpoints and meeting points up to date.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void dec_sync_settle(DecArgs a, const uint32_t* last_changed,
-                                                      const uint32_t* fchanged, uint32_t* settled) {
+constexpr uint32_t SETTLE_THREADS = 512;
+__global__ __launch_bounds__(SETTLE_THREADS) void dec_sync_settle(DecArgs a, const uint32_t* last_changed,
+                                                                  const uint32_t* fchanged, uint32_t* settled) {
   __shared__ LutLds S;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[64 * RING_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[SETTLE_THREADS * RING_STRIDE];
+  __shared__ unsigned long long xs[SETTLE_THREADS];   // each range's exit in the current round
   const uint32_t f = blockIdx.x;
-  if (*last_changed == 0 || fchanged[f] == 0 || a.status[f] != 0) return;
+  if (*last_changed == 0 || fchanged[f] == 0 || a.status[f] != 0) return;   // block-uniform
   const uint64_t len = a.stream_len[f];
   const uint64_t D = a.data_start[f];
-  const uint32_t nc = n_chunks(len, D, a.chunk_bits);
+  const uint32_t nc = min(n_chunks(len, D, a.chunk_bits), a.max_chunks);
   if (nc < 2) return;
   load_lut(S, reinterpret_cast<const DecTables*>(a.tables) + f);
   __syncthreads();
   StreamParams SP;
   SP.load(S);
-  const uint32_t lane = threadIdx.x;
+  const uint32_t t = threadIdx.x;
+  uint32_t* wring = ring + (t & ~63u) * RING_STRIDE;
+  const uint32_t* my = ring + t * RING_STRIDE;
   const uint8_t* p = a.streams + (uint64_t)f * a.stream_stride;
   const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   const uint64_t base = (uint64_t)f * a.max_chunks;
   const uint32_t N = a.W * a.H;
   const unsigned long long hard = len * 8 + 64;
-  const uint32_t* my = ring + lane * RING_STRIDE;
-  Lane L;
-  L.pos = D;
-  L.rp = RING_W;
-  uint32_t dk = 0;
-  for (uint32_t j = 0; j + 1 < nc; ++j) {
-    const unsigned long long end = D + (unsigned long long)(j + 1) * a.chunk_bits;
-    uint32_t px = 0;
-    bool active = lane == 0;
-    for (;;) {
-      if (active && (L.pos >= end || L.pos >= hard || px > N)) active = false;
-      if (!__any(active)) break;
-      if (__any(active && !lane_ok(L))) ring_fill<false>(ring, p, len, al16, L);
-      if (active) {
-        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        const uint32_t pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
-        px = sat_add(px, pixel_count(pfx, dk));
+  const uint32_t per = (nc + SETTLE_THREADS - 1) / SETTLE_THREADS;
+  const uint32_t lo = min(t * per, nc), hi = min(lo + per, nc);   // nonempty ranges: lanes 0..k, contiguous
+  unsigned long long start = lo == 0 ? 0ull : a.entry[base + lo];
+  unsigned long long xprev = 0;   // the lane's exit of the previous round
+  bool walk = lo < hi;
+  const bool fast = !a.parse_slow && reinterpret_cast<const DecTables*>(a.tables)[f].fast;
+  for (uint32_t round = 0;; ++round) {
+    // ---- one round: the lanes with `walk` parse their range from `start`
+    Lane L;
+    L.pos = D;
+    L.rp = RING_W;
+    L.ws = (uint32_t)(D >> 5) - RING_W;
+    uint32_t j = lo, dk = 0, px = 0;
+    unsigned long long end = 0, xout = xprev;
+    bool refill = true;
+    // position the lane at slice j with entry x, after the slices it may skip;
+    // false once the walk is done (xout set)
+    auto advance = [&](unsigned long long x) -> bool {
+      for (;;) {
+        if (j >= hi) { xout = x; return false; }
+        const unsigned long long cur = j == 0 ? 0ull : a.entry[base + j];
+        if (round == 0) {
+          const unsigned long long lj = a.last[base + j];
+          if (x == cur && lj != ~0ull && (lj & PS_MASK) == cur) {   // consistent: its exit is the next entry
+            x = j + 1 < nc ? a.entry[base + j + 1] : 0ull;
+            ++j;
+            continue;
+          }
+        } else if (j > lo && x == cur) {   // the rest of the range is consistent from here
+          xout = xprev;
+          return false;
+        }
+        if (j > lo) a.entry[base + j] = x;
+        L.pos = D + (x & ((1ull << 40) - 1));
+        dk = (uint32_t)(x >> 44) & 127u;
+        px = 0;
+        end = D + (unsigned long long)(j + 1) * a.chunk_bits;
+        refill = true;
+        return true;
       }
+    };
+    bool active = walk && advance(start);
+    auto parse = [&](auto fast_tag) {
+      constexpr bool FAST = decltype(fast_tag)::value;
+      StreamParams G = SP;
+      if constexpr (FAST) {
+#pragma unroll
+        for (int i = 0; i < N_STREAMS; ++i) G.g[i] = fast_param(G.g[i]);
+      }
+      for (;;) {
+        // at a prefix position: the slice's end (same stop rule as dec_sync), or one more pixel event
+        if (active && (L.pos >= end || L.pos >= hard || px > N)) {
+          ++j;
+          active = advance(ps_pack(L.pos - D, dk));
+        }
+        if (!__any(active)) break;
+        if (__any(active && (refill || !(FAST ? lane_ok_fast(L) : lane_ok(L))))) {
+          ring_fill<FAST>(wring, p, len, al16, L);
+          refill = false;
+        }
+        if (active) {
+          uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+          const uint32_t pfx = FAST ? pixel_event_fast(L, my, S, G, s0, s1, s2, s3)
+                                    : pixel_event(L, my, S, G, s0, s1, s2, s3);
+          px = sat_add(px, pixel_count(pfx, dk));
+        }
+      }
+    };
+    if (fast) parse(std::true_type{});
+    else parse(std::false_type{});
+    xs[t] = xout;
+    __syncthreads();
+    // ---- a range whose start is not its left neighbour's exit walks again
+    const unsigned long long want = (t == 0 || lo >= hi) ? start : xs[t - 1];
+    xprev = xout;
+    walk = want != start;
+    if (walk) {
+      start = want;
+      a.entry[base + lo] = want;   // lane t - 1 reads it only in round 0
     }
-    if (lane == 0) a.entry[base + j + 1] = ps_pack(L.pos - D, dk);
+    if (!__syncthreads_or(walk)) break;
   }
-  if (lane == 0) *settled = 1u;
+  if (t == 0) *settled = 1u;
 }
 
 // ---------------------------------------------------------------------------
@@ -870,6 +958,10 @@ __global__ __launch_bounds__(1024) void dec_scan(DecArgs a) {
   __shared__ unsigned long long part[1024];
   const uint32_t f = blockIdx.x;
   if (a.status[f] != 0) return;
+  if (a.unsettled && a.unsettled[f]) {   // the parse is not at its fixpoint: fail, never decode from it
+    if (threadIdx.x == 0) set_status(&a.status[f], NICE_E_HIP);
+    return;
+  }
   const uint32_t nc = n_chunks(a.stream_len[f], a.data_start[f], a.chunk_bits);
   const uint64_t base = (uint64_t)f * a.max_chunks;
   const uint32_t per = (nc + 1023) / 1024;
@@ -2341,6 +2433,11 @@ constexpr uint32_t FLOW_SLOTS = 8;   // stamp slots
 
 constexpr uint32_t FLOW_MAXW = 4;
 constexpr unsigned long long FLOW_TIMEOUT = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
+// a timed-out wait (the workgroup preempted or time-sliced for longer than
+// that) does not fail the frame: it is marked for the barrier kernel
+// (dec_rows, launched after this one in redo mode) -- slower,
+// never wrong
+constexpr int FLOW_REDO = 1;
 struct FlowCtl {
   uint32_t fin[FLOW_SLOTS][FLOW_MAXW];
   uint32_t tst[FLOW_SLOTS][FLOW_MAXW];
@@ -2379,7 +2476,7 @@ __device__ __forceinline__ bool flow_wait(FlowCtl& C, const uint32_t* stamps, ui
       if (n == 0) t0 = t;
       else if (t - t0 > FLOW_TIMEOUT) {
         atomicOr(&C.abort, 1u);
-        atomicCAS(&C.err, 0, NICE_E_HIP);
+        atomicCAS(&C.err, 0, FLOW_REDO);
         return false;
       }
     }
@@ -2463,6 +2560,9 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   const uint32_t nseg = (W + S - 1) / S, WPR = (nseg + 63) / 64, K = a.flow_k;
   const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   if (wid >= K * WPR) return;   // no barrier below this point
+  // tests (NICE_OPT_TEST_FLOW_ABSENT): the block's last wave never starts, as
+  // if it were not resident, so the others' waits time out into the fallback
+  if (a.test_absent_strip && wid == K * WPR - 1) return;
   const uint32_t g = wid / WPR, w = wid - g * WPR, lastw = WPR - 1;
   const uint32_t seg = w * 64u + lane;
   const bool active = seg < nseg;
@@ -2642,7 +2742,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
           if (t0 == 0) t0 = t;
           else if (t - t0 > FLOW_TIMEOUT) {
             atomicOr(&C.abort, 1u);
-            atomicCAS(&C.err, 0, NICE_E_HIP);
+            atomicCAS(&C.err, 0, FLOW_REDO);
             ok = false;
             break;
           }
@@ -2719,7 +2819,8 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
   }
   if (lane == 0) {
     const int e = __hip_atomic_load(&C.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (e) set_status(&a.status[f], e);
+    if (e == FLOW_REDO && a.hand_abort) atomicCAS(&a.hand_abort[f], 0u, SPLIT_REDO);
+    else if (e) set_status(&a.status[f], e == FLOW_REDO ? NICE_E_HIP : e);
   }
 #ifdef NICE_FLOW_STATS
   if (lane == 0 && a.stats) {

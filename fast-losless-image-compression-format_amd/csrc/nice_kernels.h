@@ -215,6 +215,9 @@ struct DecArgs {
   uint32_t test_absent_strip;
   // dec_rows_flow: row groups per block (rows in flight), ring rows (4 or 8)
   uint32_t flow_k, flow_ring;
+  // dec_scan: per-frame flags of the last sync iteration (an entry still moved:
+  // the frame fails with NICE_E_HIP), or null
+  const uint32_t* unsettled;
 };
 constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
 // event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =

@@ -122,3 +122,54 @@ def make_stream(O, seed, W=None, H=None, deep=None, deep_lo=25, deep_hi=31, zero
     tail = bytes(rng.integers(0, 256, int(rng.integers(0, 6)), dtype=np.uint8)) + bytes(5)
     info = {"W": W, "H": H, "deep": deep, "max": int(lens[deep].max())}
     return hdr + b.tobytes() + tail, info
+
+
+def make_slow_sync(O, seed, W, H, every=20):
+    """A stream whose Huffman parse re-synchronises only after thousands of
+    bits (the Jacobi fixpoint of the slice-parallel parse then needs tens of
+    iterations).  Every pixel is RGB with zero residuals except one pixel in
+    about `every` (SMALL_DIFF, a random index): the prefix table gives RGB the
+    1-bit code 0 and the RGB table is uniform (eight bits, code(0) = 0), so a
+    zero pixel is 25 zero bits and a parse that starts at the wrong bit keeps
+    reading 25-bit zero events at that offset; only the SMALL_DIFF pixels can
+    move it, and each lands it on the true boundary with probability about
+    1/25.  Returns the stream (header channels 3)."""
+    rng = np.random.default_rng(seed)
+    N = W * H
+    lens = []
+    for st, n in enumerate(SIZES):
+        if st == 0:
+            counts = np.full(n, 1000, np.uint64)              # uniform: every RGB code 8 bits
+        elif st == 1:
+            counts = rng.integers(1, 60, n).astype(np.uint64)
+            counts[1] = 1 << 20                               # RGB prefix: 1 bit
+        else:
+            counts = rng.integers(1, 60, n).astype(np.uint64)
+        lens.append(O.code_lengths(counts))
+    codes = [O.canonical(l) for l in lens]
+    assert int(lens[1][1]) == 1 and int(codes[1][1]) == 0
+    assert (lens[0] == 8).all() and int(codes[0][0]) == 0
+    head = _Bits()
+    for st in range(10):
+        head.put(int(lens[st].max()), 5)
+        for v in lens[st]:
+            head.put(int(v), 7)
+    # events: 25 zero bits, or SMALL_DIFF (prefix 3, index) at the breakers
+    brk = np.zeros(N, bool)
+    brk[1:] = rng.random(N - 1) < 1.0 / every
+    idx = rng.integers(0, 343, N)
+    ev_len = np.where(brk, int(lens[1][3]) + lens[5][idx].astype(np.int64), 25)
+    start = np.concatenate([[0], np.cumsum(ev_len)])
+    extra = 0   # the extra prefix the reference reads after the last pixel (code.rs:660): RGB, '0'
+    bits = np.zeros(int(start[-1]) + 1 + extra, np.uint8)
+    pc, pl = int(codes[1][3]), int(lens[1][3])
+    for i in np.nonzero(brk)[0]:
+        v = (pc << int(lens[5][idx[i]])) | int(codes[5][idx[i]])
+        n = pl + int(lens[5][idx[i]])
+        b0 = int(start[i])
+        bits[b0:b0 + n] = [(v >> (n - 1 - k)) & 1 for k in range(n)]
+    allbits = np.concatenate([np.array(head.bits, np.uint8), bits])
+    allbits = np.concatenate([allbits, np.zeros(-len(allbits) % 8, np.uint8)])
+    hdr = b"nice" + W.to_bytes(4, "big") + H.to_bytes(4, "big") + bytes([3])
+    s = hdr + np.packbits(allbits).tobytes() + bytes(5)
+    return s

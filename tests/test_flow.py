@@ -35,7 +35,7 @@ def _decode(nice, s, C):
 
 
 @pytest.mark.parametrize("W", [64, 66, 1025, 1026, 1040, 1921, 2050, 3073, 3840, 4096])
-def test_flow_widths(nice, O, W, monkeypatch):
+def test_flow_widths(nice, O, W, opts):
     H = 40
     for C in (3, 4):
         px = _frame(O, W, H, C, W + C)
@@ -47,11 +47,11 @@ def test_flow_widths(nice, O, W, monkeypatch):
             continue   # tables outside the decodable domain (see test_width_sweep)
         assert np.array_equal(ref, rgb)
         for k in ("0", "1", "2", "3", "4"):
-            monkeypatch.setenv("NICE_DEC_FLOW", k)
+            opts.setenv("NICE_DEC_FLOW", k)
             assert np.array_equal(_decode(nice, s, C), rgb), (W, C, k)
 
 
-def test_flow_batch(nice, O, monkeypatch):
+def test_flow_batch(nice, O, opts):
     """Several frames in one call (one block per frame), RGBA in, RGB and RGBA out."""
     import torch
     W, H, n = 1920, 64, 6
@@ -65,7 +65,7 @@ def test_flow_batch(nice, O, monkeypatch):
     st = st.to(dev)
     ln = torch.tensor([len(s) for s in streams], dtype=torch.int64, device=dev)
     for k in ("2", "0"):
-        monkeypatch.setenv("NICE_DEC_FLOW", k)
+        opts.setenv("NICE_DEC_FLOW", k)
         for oc in (3, 4):
             out = torch.zeros((n, W * H * oc), dtype=torch.uint8, device=dev)
             status = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -77,3 +77,52 @@ def test_flow_batch(nice, O, monkeypatch):
                 got = o[i].reshape(-1, oc)[:, :3].reshape(-1)
                 want = frames[i].reshape(-1, 4)[:, :3].reshape(-1)
                 assert np.array_equal(got, want), (k, oc, i)
+
+
+def test_flow_tall_ragged(nice, O, opts):
+    """1283 x 719 (81 segments: a second wave of 17 lanes, W % 16 = 3; the shape
+    tests/test_abi.py's C++ round trip uses) through both row-group counts.  A
+    rejected round-5 variant of the kernel's waits (head stamps, never shipped)
+    decoded this shape wrong (gpurun_out/r05za) while the narrower widths above
+    passed; the shipped kernel must keep it exact."""
+    W, H = 1283, 719
+    for C in (3, 4):
+        px = _frame(O, W, H, C, 7 + C)
+        s = O.encode(px, W, H, C)
+        rgb = px.reshape(-1, C)[:, :3].reshape(-1)
+        for k in ("1", "2"):
+            opts.setenv("NICE_DEC_FLOW", k)
+            assert np.array_equal(_decode(nice, s, C), rgb), (C, k)
+
+
+@pytest.mark.parametrize("k", ["1", "2"])
+def test_flow_timeout_falls_back(nice, O, opts, k):
+    """a wait that times out (0.2 s: the workgroup was preempted or
+    time-sliced) sends the frame to the barrier kernel instead of failing it.
+    NICE_TEST_FLOW_ABSENT makes the block's last wave return at entry, so the
+    waves waiting on it time out; the frame must still decode exactly, status 0,
+    and be counted as redone."""
+    import ctypes
+    import torch
+    W, H = 1920, 48
+    px = _frame(O, W, H, 4, 3)
+    s = O.encode(px, W, H, 4)
+    dev = torch.device("cuda", 0)
+    st = torch.from_numpy(np.frombuffer(s + bytes(-len(s) % 256), np.uint8).copy()).view(1, -1).to(dev)
+    ln = torch.tensor([len(s)], dtype=torch.int64, device=dev)
+    out = torch.zeros((1, W * H * 4), dtype=torch.uint8, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctx = nice.Context(0)
+    opts.setenv("NICE_DEC_FLOW", k)
+    opts.setenv("NICE_TEST_FLOW_ABSENT", 1)
+    nice.decode_batch(st, ln, W, H, 4, out, status, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(status[0]) == 0
+    got = out[0].view(-1, 4)[:, :3].cpu().numpy().reshape(-1)
+    assert np.array_equal(got, px.reshape(-1, 4)[:, :3].reshape(-1))
+    L = nice.lib()
+    L.nice_test_split_redos.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
+    nf, nr = ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.nice_test_split_redos(ctx.ptr, ctypes.byref(nf), ctypes.byref(nr)) == 0
+    assert (nf.value, nr.value) == (1, 1)

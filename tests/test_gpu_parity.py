@@ -100,13 +100,13 @@ def test_decode_matches(nice, O, case):
 
 
 @pytest.mark.parametrize("parse", ["fast", "general"])
-def test_decode_parse_paths(nice, O, parse, monkeypatch):
+def test_decode_parse_paths(nice, O, parse, opts):
     """dec_sync decodes a frame whose codes all fit the first-level tables and
     whose pixel events fit 64 bits from one window per event (DecTables::fast),
     others symbol by symbol with refills and the long-code search; forcing the
     general path (NICE_DEC_SLOW_PARSE) must give the same pixels."""
     if parse == "general":
-        monkeypatch.setenv("NICE_DEC_SLOW_PARSE", "1")
+        opts.setenv("NICE_DEC_SLOW_PARSE", "1")
     for name, px, w, h, c in CASES:
         if name not in ("syn512x4", "syn1920x1080x4", "syn256x3", "odd37x23x4", "noise300x200x3",
                         "stripes700x300x3", "palette333x90x3", "wide9000x6x3"):
@@ -232,10 +232,10 @@ def test_config3_batch_64x1080p(nice, O):
 
 
 @pytest.mark.parametrize("bits", [2048, 16384])
-def test_decode_long_slices(nice, O, bits, monkeypatch):
+def test_decode_long_slices(nice, O, bits, opts):
     """Long parse slices: emission runs from checkpoint sub-slices (the default
     picks them only for large batches)."""
-    monkeypatch.setenv("NICE_DEC_SLICE_BITS", str(bits))
+    opts.setenv("NICE_DEC_SLICE_BITS", str(bits))
     for name, px, w, h, c in CASES:
         if name not in ("syn512x4", "syn1920x1080x4", "stripes700x300x3", "noise300x200x3"):
             continue
@@ -254,11 +254,11 @@ def test_decode_long_slices(nice, O, bits, monkeypatch):
 @pytest.mark.parametrize("mode", [("NICE_DEC_NO_EVENTS", "1"), ("NICE_DEC_EV_CAP", "16"),
                                   ("NICE_DEC_EV_CAP", "64")])
 @pytest.mark.parametrize("bits", [1024, 4096])
-def test_decode_event_paths(nice, O, mode, bits, monkeypatch):
+def test_decode_event_paths(nice, O, mode, bits, opts):
     """Record emission without the first pass's events (every slice parsed again)
     and with a capacity so small that most slices overflow (mixed paths)."""
-    monkeypatch.setenv(*mode)
-    monkeypatch.setenv("NICE_DEC_SLICE_BITS", str(bits))
+    opts.setenv(*mode)
+    opts.setenv("NICE_DEC_SLICE_BITS", str(bits))
     for name, px, w, h, c in CASES:
         if name not in ("syn512x4", "syn1920x1080x4", "stripes700x300x3", "noise300x200x3", "odd37x23x4"):
             continue
@@ -274,9 +274,9 @@ def test_decode_event_paths(nice, O, mode, bits, monkeypatch):
         assert np.array_equal(g[:, :3].reshape(-1), px.reshape(-1, c)[:, :3].reshape(-1)), (name, mode, bits)
 
 
-def test_decode_single_wave_rows(nice, O, monkeypatch):
+def test_decode_single_wave_rows(nice, O, opts):
     """The single-wave row kernel (used for W < 64 or W > 16384) on wide images."""
-    monkeypatch.setenv("NICE_DEC_SINGLE_WAVE", "1")
+    opts.setenv("NICE_DEC_SINGLE_WAVE", "1")
     for name, px, w, h, c in CASES:
         if name not in ("syn512x4", "odd37x23x4", "palette333x90x3"):
             continue

@@ -60,12 +60,12 @@ def test_pipe_bad_stream_status(nice, O):
     assert np.array_equal(outs[0], f)
 
 
-def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
+def test_pipe_decode_unsettled_chunks_redone(nice, O, opts):
     """One queued sync iteration per chunk: the parse of long slices has not
     settled after it, so the device settle (dec_sync_settle: a sequential parse
     of the frames still changing) and the iteration behind it must give the
     fixpoint -- exact pixels, no host check."""
-    monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
+    opts.setenv("NICE_DEC_SYNC_QUEUED", "1")
     w, h, c, n = 640, 480, 4, 9
     frames = _frames(O, n, w, h, c, seed0=40)
     p = nice.Pipeline(w, h, c, batch=2, depth=2)
@@ -78,10 +78,10 @@ def test_pipe_decode_unsettled_chunks_redone(nice, O, monkeypatch):
     p.close()
 
 
-def test_pipe_decode_unsettled_with_bad_stream(nice, O, monkeypatch):
+def test_pipe_decode_unsettled_with_bad_stream(nice, O, opts):
     """The settle path with an error in a settled chunk: every good frame
     exact, the bad frame's status an error (its pixels are undefined, nice.h)."""
-    monkeypatch.setenv("NICE_DEC_SYNC_QUEUED", "1")
+    opts.setenv("NICE_DEC_SYNC_QUEUED", "1")
     w, h, c, n = 640, 480, 4, 5
     frames = _frames(O, n, w, h, c, seed0=60)
     p = nice.Pipeline(w, h, c, batch=2, depth=2)

@@ -28,9 +28,9 @@ def _frame(O, W, H, seed):
 
 @pytest.mark.parametrize("seg", ["16", "8"])
 @pytest.mark.parametrize("W", [1601, 1602, 1600, 1615])
-def test_wrap_to_current_row(nice, O, W, seg, monkeypatch):
-    monkeypatch.setenv("NICE_DEC_SEG", seg)
-    monkeypatch.setenv("NICE_DEC_SPLIT", "0")
+def test_wrap_to_current_row(nice, O, W, seg, opts):
+    opts.setenv("NICE_DEC_SEG", seg)
+    opts.setenv("NICE_DEC_SPLIT", "0")
     H = 48
     px = _frame(O, W, H, 0)
     s = O.encode(px, W, H, 3)

@@ -41,25 +41,25 @@ def _check(nice, O, px, w, h, c):
 
 
 @pytest.mark.parametrize("k", [2, 3, 5])
-def test_split_forced_strips(nice, O, k, monkeypatch):
-    monkeypatch.setenv("NICE_DEC_SPLIT", str(k))
+def test_split_forced_strips(nice, O, k, opts):
+    opts.setenv("NICE_DEC_SPLIT", str(k))
     for name, px, w, h, c in _cases(O):
         assert _check(nice, O, px, w, h, c), (name, k)
 
 
-def test_split_default_wide(nice, O, monkeypatch):
+def test_split_default_wide(nice, O, opts):
     """W > 4096 splits by default (ceil(W / 16 / 256) strips); =0 disables."""
     px = O.gen_syn_v1(8200, 9, 4, 8)
     assert _check(nice, O, px, 8200, 9, 4)
-    monkeypatch.setenv("NICE_DEC_SPLIT", "0")
+    opts.setenv("NICE_DEC_SPLIT", "0")
     assert _check(nice, O, px, 8200, 9, 4)
 
 
-def test_split_batch_rgb_out(nice, O, monkeypatch):
+def test_split_batch_rgb_out(nice, O, opts):
     """A batch (several frames, each split) through the device API, RGBA
     streams decoded to 3-channel output."""
     import torch
-    monkeypatch.setenv("NICE_DEC_SPLIT", "3")
+    opts.setenv("NICE_DEC_SPLIT", "3")
     w, h, c, n = 1200, 20, 4, 5
     frames = [O.gen_syn_v1(w, h, c, 30 + i) for i in range(n)]
     streams = [O.encode(f, w, h, c) for f in frames]
@@ -78,11 +78,11 @@ def test_split_batch_rgb_out(nice, O, monkeypatch):
         assert np.array_equal(dec[i].cpu().numpy(), frames[i].reshape(-1, 4)[:, :3].reshape(-1)), i
 
 
-def test_split_corrupt_stream_fails_fast(nice, O, monkeypatch):
+def test_split_corrupt_stream_fails_fast(nice, O, opts):
     """A stream whose records reference outside the image or mis-parse: the
     split decode reports an error (or decodes) without waiting on a strip that
     stopped -- it returns well inside the per-row poll timeout."""
-    monkeypatch.setenv("NICE_DEC_SPLIT", "4")
+    opts.setenv("NICE_DEC_SPLIT", "4")
     w, h, c = 1500, 30, 3
     px = O.gen_syn_v1(w, h, c, 12)
     s = bytearray(O.encode(px, w, h, c))
@@ -101,11 +101,11 @@ def test_split_corrupt_stream_fails_fast(nice, O, monkeypatch):
 
 
 @pytest.mark.parametrize("seg", ["8", "16"])
-def test_row_segment_sizes(nice, O, seg, monkeypatch):
+def test_row_segment_sizes(nice, O, seg, opts):
     """dec_rows8 (8-pixel segments, on request since round 4) and dec_rows (16)
     forced on the same frames: identical pixels."""
-    monkeypatch.setenv("NICE_DEC_SEG", seg)
-    monkeypatch.setenv("NICE_DEC_SPLIT", "0")
+    opts.setenv("NICE_DEC_SEG", seg)
+    opts.setenv("NICE_DEC_SPLIT", "0")
     for name, px, w, h, c in _cases(O) + [("syn64x9x3", O.gen_syn_v1(64, 9, 3, 2), 64, 9, 3),
                                           ("syn2047x12x4", O.gen_syn_v1(2047, 12, 4, 3), 2047, 12, 4)]:
         assert _check(nice, O, px, w, h, c), (name, seg)
@@ -200,7 +200,7 @@ def test_split_not_coresident_falls_back(nice, O):
 
 
 @pytest.mark.parametrize("shape", [(16384, 64, 4), (20000, 24, 3)], ids=["16384x64x4", "20000x24x3"])
-def test_split_absent_strip_redone(nice, O, shape, monkeypatch):
+def test_split_absent_strip_redone(nice, O, shape, opts):
     """A strip that never becomes resident (test hook split_absent: the last
     strip of each frame returns at entry): its neighbour's halo wait times out
     (0.2 s), the frame's strips stop, and the fallback launch (dec_rows_wide;

@@ -49,8 +49,8 @@ def _same(got, want, what):
 
 
 @pytest.mark.parametrize("group", list(WIDTHS))
-def test_width_sweep(nice, O, group, monkeypatch):
-    monkeypatch.setenv("NICE_DEC_SEG", "16")
+def test_width_sweep(nice, O, group, opts):
+    opts.setenv("NICE_DEC_SEG", "16")
     for W in WIDTHS[group]:
         for C in (3, 4):
             px = _frame(O, W, C, W * 7 + C)
@@ -72,8 +72,8 @@ def test_width_sweep(nice, O, group, monkeypatch):
                         nice.decode_bytes(want, flags=nice.DEC_TOLERANT_HEADER | nice.DEC_ALPHA_FILL_FF)
                 continue
             for seg in ("16", "8"):
-                monkeypatch.setenv("NICE_DEC_SEG", seg)
+                opts.setenv("NICE_DEC_SEG", seg)
                 got, img = nice.decode_bytes(want, flags=nice.DEC_TOLERANT_HEADER | nice.DEC_ALPHA_FILL_FF)
                 g = np.frombuffer(got, np.uint8).reshape(-1, C)
                 assert np.array_equal(g[:, :3].reshape(-1), rgb), (W, C, seg)
-            monkeypatch.setenv("NICE_DEC_SEG", "16")
+            opts.setenv("NICE_DEC_SEG", "16")

@@ -3,6 +3,9 @@ import importlib, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import opts as _opts  # noqa: E402
+_opts.apply_env(nice)
 from oracle import oracle as O
 w, h = int(os.environ.get("W", 3840)), int(os.environ.get("H", 2160))
 px = O.gen_syn_v1(w, h, 4, 1)

@@ -5,6 +5,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import bench
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import opts as _opts  # noqa: E402
+_opts.apply_env(nice)
 W, H, n = 3840, 2160, int(os.environ.get("NF", 256))
 tag = os.environ.get("NICE_LIB_PATH", "in-tree")
 dev = torch.device("cuda", 0)

@@ -5,6 +5,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import bench
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import opts as _opts  # noqa: E402
+_opts.apply_env(nice)
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 W = int(sys.argv[3]) if len(sys.argv) > 4 else 3840

@@ -7,6 +7,8 @@ sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import oracle as O
 from test_width_sweep import _frame, H as H0
 nice = importlib.import_module("fast-losless-image-compression-format_amd")
+from conftest import Opts
+opts = Opts(nice)
 w0, w1 = int(sys.argv[1]), int(sys.argv[2])
 H = int(sys.argv[3]) if len(sys.argv) > 3 else H0
 import test_width_sweep as T
@@ -19,9 +21,9 @@ for W in range(w0, w1):
         res = []
         for name, env in [("seg16", {"NICE_DEC_SEG": "16"}), ("seg8", {"NICE_DEC_SEG": "8"}),
                           ("single", {"NICE_DEC_SINGLE_WAVE": "1"}), ("slow", {"NICE_DEC_SLOW_PARSE": "1"})]:
-            for k in ("NICE_DEC_SEG", "NICE_DEC_SINGLE_WAVE", "NICE_DEC_SLOW_PARSE"):
-                os.environ.pop(k, None)
-            os.environ.update(env)
+            opts.reset()
+            for k, v in env.items():
+                opts.setenv(k, v)
             try:
                 got, _ = nice.decode_bytes(s, flags=nice.DEC_TOLERANT_HEADER | nice.DEC_ALPHA_FILL_FF)
                 g = np.frombuffer(got, np.uint8).reshape(-1, C)[:, :3]
