@@ -323,11 +323,15 @@ static uint32_t strip_rows(const nice_ctx* ctx, uint32_t n_frames, uint32_t w, u
 // window kernel for pixel memory that is not 4-byte aligned.  `aligned`: the
 // pixel base (frames: and stride) is 4-byte aligned, as the ring, strip and
 // tile-window loads need.
-enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR, CLS_K_TWIN };
-static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
+// `frames_al16` (frames, not a band; pixel base and frame stride 16-byte
+// aligned): the per-lane sliding-window kernel for RGBA rows that fit the ring.
+enum ClsKind { CLS_K_WINDOW, CLS_K_TINY, CLS_K_RING, CLS_K_RING2, CLS_K_STRIP, CLS_K_PAIR, CLS_K_TWIN, CLS_K_SLIDE };
+static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned, bool frames_al16 = false) {
   if (w < 3) return CLS_K_TINY;
   if (!aligned || opt_on(NICE_OPT_ENC_NO_RING)) return CLS_K_WINDOW;
   const bool no_pair = opt_on(NICE_OPT_ENC_NO_PAIR);   // A/B: one tile per iteration
+  if (channels == 4 && w <= CLS_PAIR_MAX_W && frames_al16 && !no_pair && !opt_on(NICE_OPT_ENC_NO_SLIDE))
+    return CLS_K_SLIDE;
   if (channels == 4 && w <= CLS_PAIR_MAX_W && !no_pair) return CLS_K_PAIR;
   if (w <= CLS_RING_MAX_W) return CLS_K_RING;
   if (channels == 4 && w % ENC_TILE == 0) return CLS_K_STRIP;
@@ -338,11 +342,11 @@ static ClsKind pick_classify(uint32_t w, uint8_t channels, bool aligned) {
 // strip kernel walks per frame.
 static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work, uint32_t rows_total,
                             hipStream_t st) {
-  const bool ringk = k == CLS_K_RING || k == CLS_K_RING2 || k == CLS_K_PAIR;
+  const bool ringk = k == CLS_K_RING || k == CLS_K_RING2 || k == CLS_K_PAIR || k == CLS_K_SLIDE;
   // contiguous tile chunks per block: keeps rows-above reuse in L2 and flushes
   // each block's LDS histogram once per frame; ring kernels: >= 16 tiles per
   // block (the 3-row prefill amortised), 2 blocks per CU (ring2: 1)
-  uint64_t blocks = (k == CLS_K_RING || k == CLS_K_PAIR) ? 2ull * ctx->cus : k == CLS_K_RING2 ? (uint64_t)ctx->cus : 2048;
+  uint64_t blocks = (k == CLS_K_RING || k == CLS_K_PAIR || k == CLS_K_SLIDE) ? 2ull * ctx->cus : k == CLS_K_RING2 ? (uint64_t)ctx->cus : 2048;
   uint64_t per = (work + blocks - 1) / blocks;
   if (per < (ringk ? 16u : 1u)) per = ringk ? 16 : 1;
   if (ringk && per > 16384) per = 16384;   // its 16-bit per-thread prefix counters
@@ -368,6 +372,16 @@ static void launch_classify(nice_ctx* ctx, ClsKind k, EncArgs& a, uint64_t work,
       if (a.cmask) hipLaunchKernelGGL(enc_classify_pair_m, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       else hipLaunchKernelGGL(enc_classify_pair, dim3((uint32_t)blocks), dim3(CLS_THREADS_HOST), 0, st, a);
       break;
+    case CLS_K_SLIDE: {   // frames only (coded flags out in ballot order)
+      const dim3 g((uint32_t)blocks), b(CLS_THREADS_HOST);
+      switch (a.W & 3u) {
+        case 0: hipLaunchKernelGGL(enc_classify_slide0, g, b, 0, st, a); break;
+        case 1: hipLaunchKernelGGL(enc_classify_slide1, g, b, 0, st, a); break;
+        case 2: hipLaunchKernelGGL(enc_classify_slide2, g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL(enc_classify_slide3, g, b, 0, st, a); break;
+      }
+      break;
+    }
     case CLS_K_RING2:
       if (rgb) hipLaunchKernelGGL(a.cmask ? enc_classify_ring2_3_m : enc_classify_ring2_3, dim3((uint32_t)blocks),
                                   dim3(CLS_THREADS_HOST), 0, st, a);
@@ -411,7 +425,8 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
   const uint32_t T = tiles_for(w, h);
   // one frame: its stride is never applied (an odd W*H*3 RGB stride is fine)
   const bool aligned = ((uintptr_t)d_px & 3) == 0 && (n_frames == 1 || (frame_stride & 3) == 0);
-  const ClsKind ck = pick_classify(w, channels, aligned);
+  const bool al16 = ((uintptr_t)d_px & 15) == 0 && (n_frames == 1 || (frame_stride & 15) == 0);
+  const ClsKind ck = pick_classify(w, channels, aligned, al16);
   if ((uint64_t)n_frames * T >= (1ull << 32)) return NICE_E_ARG;   // enc_pack's 32-bit work counter
   EncLayout L = enc_layout(n_frames, T, N);
   int rc = ctx->enc.grow(L.total);
@@ -433,7 +448,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
     if (ck != CLS_K_WINDOW && ck != CLS_K_TINY)   // in-tile run digits, from the coded flags
       hipLaunchKernelGGL(enc_rundigits,
                          dim3(std::min<uint32_t>((T + 7) / 8, std::max<uint32_t>(64u, 2048u / n_frames)), n_frames),
-                         dim3(256), 0, st, a);   // (>= 2048 blocks in all for few, large frames)
+                         dim3(256), 0, st, a, ck == CLS_K_SLIDE ? 1 : 0);   // (>= 2048 blocks in all for few, large frames)
     ctx->last_classify = (int)ck;
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
@@ -1326,7 +1341,8 @@ int nice_test_occupy(void* stream, uint32_t blocks, uint32_t short_blocks, uint3
   return NICE_OK;
 }
 // The classify kernel the context's last encode (or band classify) used:
-// 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip, 5 pair (two tiles per iteration).
+// 0 window, 1 tiny, 2 ring, 3 ring2 (32K ring), 4 strip, 5 pair (two tiles per iteration),
+// 6 twin (per-tile row windows), 7 slide (per-lane sliding windows).
 int nice_test_last_classify(nice_ctx* ctx) { return ctx ? ctx->last_classify : -1; }
 
 // Test hooks of one context (tests only; nothing reads the environment for them):

@@ -1141,6 +1141,308 @@ __global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_pair_m(EncArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// K1w: classify with per-lane sliding windows (round 6; RGBA frames, 3 <= W <=
+// CLS_PAIR_MAX_W, pixel memory 16-byte aligned: the bench path).  The pair
+// kernel gives each lane pixels 512 apart, so every pixel re-reads its 13
+// neighbours from the ring one word at a time (about 15 LDS instructions and
+// three Y -> RGB conversions per pixel).  Here a lane owns 4 CONSECUTIVE
+// pixels of the iteration's 2048 (one 16-byte global load, one 16-byte ring
+// store) and reads, per neighbour row, one aligned window covering its 4
+// pixels' references (rows y-1 and y-3: pixels i-rW-3 .. i-rW+6; row y-2:
+// i-2W .. i-2W+3; row y: the 3 pixels before) with ds_read_b128s -- 8 to 11
+// per 4 pixels, conflict-free (consecutive lanes read consecutive 16 bytes).
+// Every reference is then a register chosen at compile time: the window
+// offsets depend only on W mod 4 (the template parameter), the left
+// neighbours L, L2, L3 of pixels 1..3 are the lane's own pixels, and pixel
+// q's RGB spread is pixel q+1's RGB(L) (one conversion saved per pixel).
+// The coded flags come out of the compares as wave ballots; the per-tile
+// first / last coded pixel are found from them with scalar bit scans, and the
+// flags go to a.cmask in the ballot order (wave w's 8 words: ballot q's low
+// and high halves), which enc_rundigits transposes.  Same records, histogram
+// and tile edges as enc_classify_pair_m (code.rs:159-414).
+// ---------------------------------------------------------------------------
+// pixel word v (R | G << 8 | B << 16) -> its Y-space value and RGB spread (sharing G)
+__device__ __forceinline__ void y_rgb_from_rgba(uint32_t v, uint32_t& y, uint32_t& xr) {
+  const uint32_t g = __builtin_amdgcn_ubfe(v, 8, 8);
+  const nice_u16x2 d = __builtin_bit_cast(nice_u16x2, v) - __builtin_bit_cast(nice_u16x2, g | (g << 16));
+  const uint32_t t = __builtin_bit_cast(uint32_t, d);
+  y = (__umul24(t & 0xFF0000u, 16u) + (t & 0xFFu)) | (g << 10);
+  xr = (y + __umul24(g, 0x100001u)) & K3(0xFFu);
+}
+
+// classify_y<false> with every reference in registers: X (Y space) and its RGB
+// spread xr, L and its spread lrgb; the luma hit's difference is read again from
+// the ring at (i + loff[k]) mod RING (loff[k] = -offset of reference k).
+__device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32_t L, uint32_t lrgb, uint32_t L2,
+                                                 uint32_t L3, uint32_t U, uint32_t UR1, uint32_t UR3, uint32_t UL3,
+                                                 uint32_t U2, uint32_t V, uint32_t VR1, uint32_t VL1, uint32_t VL3,
+                                                 uint32_t VR3, const uint32_t* ring, uint32_t i, const uint32_t* loff,
+                                                 uint32_t cbr, uint32_t csd) {
+  // back references k = 1..4 (code.rs:191-206)
+  const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
+  const bool br = e1 | e2 | e3 | e4;
+  const uint32_t bk = e1 ? 1u : e2 ? 2u : e3 ? 3u : 4u;
+  const uint32_t pred = avg3(rgb_from_y(U), lrgb);
+  // small diff (code.rs:208-247), as in classify_y
+  const uint32_t d = xr + K3(259u) - pred;
+  const bool sd = ((d & K3(0x3F8u)) | ((d + K3(1u)) & K3(8u))) == K3(0x100u);
+  const uint32_t sdi = (__umul24(d & K3(7u), 49u | (7u << 10) | (1u << 20)) >> 20) & 0x3FFu;
+  // luma2 (code.rs:252-292)
+  const uint32_t pg = (pred >> 10) & 0xFFu;
+  const uint32_t xk = X + LUMA_KY;
+  const uint32_t t2 = (xk - pred) + (pg | (pg << 20));
+  const bool l2 = (t2 & LUMA_MASK) == 0;
+  // luma, 11 references, first hit wins (code.rs:293-339): min-key search
+  uint32_t lk = 11u, lt = 0u;
+  if (__builtin_amdgcn_ballot_w64(!br && !sd && !l2) != 0ull) {
+    const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
+    uint32_t key[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) key[k] = ((xk - refs[k]) & LUMA_MASK) | (uint32_t)k;
+    const uint32_t m = min(min(min(min(key[0], key[1]), key[2]), min(min(key[3], key[4]), key[5])),
+                           min(min(min(key[6], key[7]), key[8]), min(key[9], key[10])));
+    lk = min(m, 11u);
+    lt = xk - ring[(i + loff[m & 15u]) & (CLS_RING - 1)];
+  }
+  const uint32_t r = d - K3(3u);   // = xr + 256 - pred per field
+  const uint32_t rec_br = (bk << 3) + cbr;
+  const uint32_t rec_sd = (sdi << 3) + csd;
+  const uint32_t rs = r & K3(0xFFu);
+  const uint32_t rec_rgb = (rs + (rs & (0xFFu << 10))) << 3;
+  const uint32_t lf = l2 ? t2 : lt;
+  const uint32_t lbase = l2 ? ((C0_L2 << 3) | (SX_L2 << 14) | (SX_L2 << 23))
+                            : ((C0_LUMA << 3) | (SX_LUMA << 14) | (SX_LUMA << 23)) + (lk << 9);
+  const uint32_t rec_lu = lbase + (__builtin_amdgcn_ubfe(lf, 10, 6) << 3) + ((lf & 0x1Fu) << 14) +
+                          ((lf & (0x1Fu << 20)) << 3);
+  return br ? rec_br : sd ? rec_sd : (l2 || lk < 11u) ? rec_lu : rec_rgb;
+}
+
+template <int WM>   // W mod 4
+__device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
+  constexpr int RING = CLS_RING;
+  constexpr uint32_t RM = RING - 1;
+  // window geometry (words, all multiples of 4 away from the lane's first
+  // pixel i0 = start + 4 tid): row r's window starts OFF_r before i0, rounded
+  // up to a multiple of 4 by D_r, and spans NB_r 16-byte blocks
+  constexpr uint32_t D1 = (4u - (uint32_t)(WM + 3) % 4u) % 4u;       // row y-1: i - W - 3 ..
+  constexpr uint32_t D2 = (4u - (uint32_t)(2 * WM) % 4u) % 4u;       // row y-2: i - 2W ..
+  constexpr uint32_t D3 = (4u - (uint32_t)(3 * WM + 3) % 4u) % 4u;   // row y-3: i - 3W - 3 ..
+  constexpr int NB1 = (int)(D1 + 10u + 3u) / 4, NB2 = (int)(D2 + 4u + 3u) / 4, NB3 = (int)(D3 + 10u + 3u) / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[RING + CLS_GUARD];
+  __shared__ uint32_t hs[C0_N + 2 * SX_N];     // slot histogram (nice_rec.hpp)
+  __shared__ uint32_t loff[16];                // luma reference k: -(its offset) mod RING
+  __shared__ uint32_t wfl[2][CLS_THREADS / 64][2];   // [parity][wave]: first coded pixel, last + 1 (tile-relative)
+  const uint64_t total_work = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
+  const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
+  const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
+  if (w_begin >= w_end) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t cbr = (C0_BR << 3) | rec2_abs(lane), csd = (C0_SD << 3) | rec2_abs(lane);
+  const uint32_t cunc = rec2_unc(lane);
+  const uint32_t W = a.W;
+  const int64_t N = (int64_t)W * a.H;
+  const uint32_t OFF1 = W + 3u + D1, OFF2 = 2u * W + D2, OFF3 = 3u * W + 3u + D3;
+  for (uint32_t b = tid; b < C0_N + 2 * SX_N; b += CLS_THREADS) hs[b] = 0;
+  if (tid < 16) loff[tid] = tid < 11 ? (0u - ((uint32_t)lr_rows((int)tid) * W + (uint32_t)lr_px((int)tid))) & RM : 0u;
+  auto flush = [&](uint32_t frame) {
+    __syncthreads();
+    for (int b = tid; b < N_BINS; b += CLS_THREADS) {
+      const uint32_t v = slot_hist_bin(hs, b);
+      if (v) atomicAdd(&a.hist[(uint64_t)frame * N_BINS + b], v);
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < C0_N + 2 * SX_N; b += CLS_THREADS) hs[b] = 0;
+  };
+  TileIter it(a, w_begin);
+  uint32_t cur_frame = it.f;
+  {   // prefill: the 3 rows + 3 pixels before the first tile
+    const int64_t start = (int64_t)it.tt() * ENC_TILE;
+    const int64_t lo = max((int64_t)0, start - 3 * (int64_t)W - 3);
+    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)cur_frame * a.frame_stride);
+    for (int64_t j = lo + tid; j < start; j += CLS_THREADS) {
+      const uint32_t k = (uint32_t)j & RM, y = y_from_rgba(fr[j]);
+      ring[k] = y;
+      if (k < CLS_GUARD) ring[RING + k] = y;
+    }
+  }
+  auto tiles_at = [&](const TileIter& ti, uint64_t w) -> int {
+    return (w + 1 < w_end && ti.k + 1 < ti.nt) ? 2 : 1;
+  };
+  uint4 pf;
+  auto fetch = [&](const TileIter& ti, int nti) {
+    const uint32_t* fr = reinterpret_cast<const uint32_t*>(a.px + (uint64_t)ti.f * a.frame_stride);
+    const int64_t j = (int64_t)ti.tt() * ENC_TILE + 4 * (int64_t)tid;
+    if (tid < 256u * (uint32_t)nti && j + 4 <= N) {
+      pf = *reinterpret_cast<const uint4*>(fr + j);
+    } else {
+      const bool in = tid < 256u * (uint32_t)nti;
+      pf.x = in && j < N ? fr[j] : 0u;
+      pf.y = in && j + 1 < N ? fr[j + 1] : 0u;
+      pf.z = in && j + 2 < N ? fr[j + 2] : 0u;
+      pf.w = in && j + 3 < N ? fr[j + 3] : 0u;
+    }
+  };
+  // the previous iteration's tiles: first / last coded pixel from its waves'
+  // entries (after a barrier)
+  uint64_t prev_tile = 0;
+  int64_t prev_start = 0;
+  uint32_t prev_cur = 0, prev_par = 0;
+  auto combine = [&]() {
+    if (tid < prev_cur) {
+      uint32_t fi = NONE, la = 0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        fi = min(fi, wfl[prev_par][4 * tid + v][0]);
+        la = max(la, wfl[prev_par][4 * tid + v][1]);
+      }
+      const int64_t sj = prev_start + (int64_t)tid * ENC_TILE;
+      a.tile_first[prev_tile + tid] = fi == NONE ? NONE : (uint32_t)(sj + fi);
+      a.tile_last[prev_tile + tid] = la == 0 ? NONE : (uint32_t)(sj + la - 1);
+    }
+  };
+  uint64_t w = w_begin;
+  int nti = tiles_at(it, w);
+  fetch(it, nti);
+  uint32_t par = 0;
+  while (w < w_end) {
+    const int cur = nti;
+    const uint32_t f = it.f;
+    if (f != cur_frame) {
+      flush(cur_frame);
+      cur_frame = f;
+    }
+    const int64_t start = (int64_t)it.tt() * ENC_TILE;
+    const int count = (int)min((int64_t)(cur * ENC_TILE), N - start);   // pixels of the iteration
+    // the lane's 4 pixels in Y space and RGB spread; into the ring
+    uint32_t X[4], XR[4];
+    y_rgb_from_rgba(pf.x, X[0], XR[0]);
+    y_rgb_from_rgba(pf.y, X[1], XR[1]);
+    y_rgb_from_rgba(pf.z, X[2], XR[2]);
+    y_rgb_from_rgba(pf.w, X[3], XR[3]);
+    const uint32_t i0 = (uint32_t)start + 4u * tid;
+    if (tid < 256u * (uint32_t)cur) {
+      const uint32_t k = i0 & RM;
+      *reinterpret_cast<uint4*>(ring + k) = make_uint4(X[0], X[1], X[2], X[3]);
+      if (k < CLS_GUARD) *reinterpret_cast<uint4*>(ring + RING + k) = make_uint4(X[0], X[1], X[2], X[3]);
+    }
+    // the next iteration's pixels, in flight during this one
+    TileIter nx = it;
+    nx.step((uint32_t)cur);
+    if (w + cur < w_end) {
+      nti = tiles_at(nx, w + cur);
+      fetch(nx, nti);
+    }
+    __syncthreads();
+    if (prev_cur) combine();
+    const bool fast = start >= 3 * (int64_t)W + 3;   // block-uniform
+    uint32_t rec[4];
+    unsigned long long bal[4];
+    if (fast) {
+      // the windows: base = ring index of (wave's first pixel - OFF_r) plus 4 lane
+      const uint32_t sw = (uint32_t)start + 256u * wave;
+      const uint32_t* b0 = ring + ((sw - 4u) & RM) + 4u * lane;
+      const uint32_t* b1 = ring + ((sw - OFF1) & RM) + 4u * lane;
+      const uint32_t* b2 = ring + ((sw - OFF2) & RM) + 4u * lane;
+      const uint32_t* b3 = ring + ((sw - OFF3) & RM) + 4u * lane;
+      uint32_t w0[4], w1[4 * NB1], w2[4 * NB2], w3[4 * NB3];
+      {
+        const uint4 v = *reinterpret_cast<const uint4*>(b0);
+        w0[0] = v.x; w0[1] = v.y; w0[2] = v.z; w0[3] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < NB1; ++b) {
+        const uint4 v = *reinterpret_cast<const uint4*>(b1 + 4 * b);
+        w1[4 * b] = v.x; w1[4 * b + 1] = v.y; w1[4 * b + 2] = v.z; w1[4 * b + 3] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < NB2; ++b) {
+        const uint4 v = *reinterpret_cast<const uint4*>(b2 + 4 * b);
+        w2[4 * b] = v.x; w2[4 * b + 1] = v.y; w2[4 * b + 2] = v.z; w2[4 * b + 3] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < NB3; ++b) {
+        const uint4 v = *reinterpret_cast<const uint4*>(b3 + 4 * b);
+        w3[4 * b] = v.x; w3[4 * b + 1] = v.y; w3[4 * b + 2] = v.z; w3[4 * b + 3] = v.w;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t L = q >= 1 ? X[q - 1] : w0[3];
+        const uint32_t L2 = q >= 2 ? X[q - 2] : w0[2 + q];
+        const uint32_t L3 = q >= 3 ? X[q - 3] : w0[1 + q];
+        const uint32_t lrgb = q >= 1 ? XR[q - 1] : rgb_from_y(w0[3]);
+        const bool coded = 4 * (int)tid + q < count && X[q] != L;
+        bal[q] = __builtin_amdgcn_ballot_w64(coded);
+        const uint32_t rf = classify_win(X[q], XR[q], L, lrgb, L2, L3, w1[q + 3 + D1], w1[q + 4 + D1],
+                                         w1[q + 6 + D1], w1[q + D1], w2[q + D2], w3[q + 3 + D3], w3[q + 4 + D3],
+                                         w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, i0 + (uint32_t)q, loff,
+                                         cbr, csd);
+        rec[q] = coded ? rf : cunc;
+      }
+    } else {
+      // the frame's first rows: the reference's validity rules (classify_y<true>)
+      // per pixel, neighbours one word at a time (s + tid: the pixel's index)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t i = i0 + (uint32_t)q;
+        const bool coded = 4 * (int)tid + q < count && (i == 0 || X[q] != ring[(i - 1u) & RM]);
+        bal[q] = __builtin_amdgcn_ballot_w64(coded);
+        const uint32_t rf = classify_ring<true>(ring, (uint32_t)start + (uint32_t)q + 3u * tid, tid, W, i, nullptr,
+                                                cbr, csd, X[q]);
+        rec[q] = coded ? rf : cunc;
+      }
+    }
+    // the wave's first / last coded pixel (tile-relative) and its coded flags
+    // in ballot order (enc_rundigits transposes them)
+    if (tid < 256u * (uint32_t)cur) {
+      uint32_t fi = NONE, la = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (bal[q]) {
+          fi = min(fi, 4u * (uint32_t)__builtin_ctzll(bal[q]) + (uint32_t)q);
+          la = max(la, 4u * (uint32_t)(63 - __builtin_clzll(bal[q])) + (uint32_t)q + 1u);
+        }
+      }
+      const uint32_t wo = 256u * (wave & 3u);
+      if (lane == 0) {
+        wfl[par][wave][0] = fi == NONE ? NONE : wo + fi;
+        wfl[par][wave][1] = la == 0 ? 0u : wo + la;
+      }
+      const uint32_t hw = lane & 1u, qq = (lane >> 1) & 3u;
+      const unsigned long long bq = qq == 0 ? bal[0] : qq == 1 ? bal[1] : qq == 2 ? bal[2] : bal[3];
+      if (lane < 8u) a.cmask[(it.tile() + (wave >> 2)) * (ENC_TILE / 32) + 8u * (wave & 3u) + lane] =
+          (uint32_t)(bq >> (32u * hw));
+    }
+    // records out, histogram
+    uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + (uint64_t)i0;
+    if (4 * (int)tid + 3 < count) {
+      *reinterpret_cast<uint4*>(recs) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * (int)tid + q < count) recs[q] = rec[q];
+    }
+    if (tid < 256u * (uint32_t)cur) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) slot_hist_add(hs, rec[q]);
+    }
+    prev_tile = it.tile();
+    prev_start = start;
+    prev_cur = (uint32_t)cur;
+    prev_par = par;
+    par ^= 1u;
+    it.step((uint32_t)cur);
+    w += (uint64_t)cur;
+  }
+  __syncthreads();
+  combine();
+  flush(cur_frame);
+}
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_slide0(EncArgs a) { enc_classify_slide_body<0>(a); }
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_slide1(EncArgs a) { enc_classify_slide_body<1>(a); }
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_slide2(EncArgs a) { enc_classify_slide_body<2>(a); }
+__global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_slide3(EncArgs a) { enc_classify_slide_body<3>(a); }
+
+// ---------------------------------------------------------------------------
 // K1r: run digits of the runs inside tiles (code.rs:371-407: a run between two
 // coded pixels of one tile, length L >= 1, adds the base-8 digits of L - 1 to
 // the run prefixes' bins; runs that cross a tile's end are enc_tailruns'),
@@ -1151,7 +1453,11 @@ __global__ __launch_bounds__(CLS_THREADS, 2) void enc_classify_pair_m(EncArgs a)
 // the previous coded pixel of the word, or the last coded pixel of the tile's
 // earlier words (a max scan over the half-wave), or none in the tile (skipped).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void enc_rundigits(EncArgs a) {
+// il != 0: the tiles' flags are in enc_classify_slide's ballot order (wave w
+// of a tile: words 8w + 2q + h = half h of the ballot of its lanes' q-th
+// pixels, pixel 256w + 4 lane + q), transposed here: standard word k holds
+// byte k % 8 of each ballot q, bit m at 4m + q.
+__global__ __launch_bounds__(256) void enc_rundigits(EncArgs a, int il) {
   __shared__ uint32_t bins[8];
   if (threadIdx.x < 8) bins[threadIdx.x] = 0;
   __syncthreads();
@@ -1161,7 +1467,23 @@ __global__ __launch_bounds__(256) void enc_rundigits(EncArgs a) {
   uint32_t cnt[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
   for (uint32_t t0 = 2u * wv; t0 < T; t0 += 2u * nwv) {   // lanes 0-31: tile t0, 32-63: tile t0 + 1
     const uint32_t t = t0 + (lane >> 5);
-    const uint32_t m = t < T ? a.cmask[((uint64_t)f * T + t) * (ENC_TILE / 32) + k] : 0u;
+    uint32_t m = 0;
+    if (t < T) {
+      if (il) {
+        const uint32_t* tw = a.cmask + ((uint64_t)f * T + t) * (ENC_TILE / 32) + 8u * (k >> 3) + ((k >> 2) & 1u);
+        const uint32_t sh = 8u * (k & 3u);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+          uint32_t x = (tw[2 * q] >> sh) & 0xFFu;   // bit m -> bit 4m
+          x = (x | (x << 12)) & 0x000F000Fu;
+          x = (x | (x << 6)) & 0x03030303u;
+          x = (x | (x << 3)) & 0x11111111u;
+          m |= x << q;
+        }
+      } else {
+        m = a.cmask[((uint64_t)f * T + t) * (ENC_TILE / 32) + k];
+      }
+    }
     // last coded pixel of the tile before this word (-1: none)
     int inc = m ? (int)(32u * k + 31u - (uint32_t)__clz((int)m)) : -1;
 #pragma unroll

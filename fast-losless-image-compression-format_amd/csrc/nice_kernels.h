@@ -102,7 +102,13 @@ __global__ void enc_classify_ring_m(EncArgs a);
 __global__ void enc_classify_ring3_m(EncArgs a);
 __global__ void enc_classify_ring2_m(EncArgs a);
 __global__ void enc_classify_ring2_3_m(EncArgs a);
-__global__ void enc_rundigits(EncArgs a);
+__global__ void enc_rundigits(EncArgs a, int il);   // il: enc_classify_slide's ballot-order flags
+// RGBA frames, 3 <= W <= CLS_PAIR_MAX_W, 16-byte aligned pixels: per-lane sliding
+// windows, one kernel per W mod 4
+__global__ void enc_classify_slide0(EncArgs a);
+__global__ void enc_classify_slide1(EncArgs a);
+__global__ void enc_classify_slide2(EncArgs a);
+__global__ void enc_classify_slide3(EncArgs a);
 // per-tile row windows (any W > CLS_RING2_MAX_W the strip kernel does not take; RGBA and RGB)
 __global__ void enc_classify_twin(EncArgs a);
 __global__ void enc_classify_twin_m(EncArgs a);

@@ -12,7 +12,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-WINDOW, TINY, RING, RING2, STRIP, PAIR, TWIN = range(7)
+WINDOW, TINY, RING, RING2, STRIP, PAIR, TWIN, SLIDE = range(8)
 
 
 def _same(got, want, what):
@@ -41,7 +41,7 @@ def _encode_dev(nice, px, w, h, c, ctx):
 
 @pytest.mark.parametrize("shape,kind", [((7680, 64, 4), RING2), ((6000, 32, 3), RING2), ((10239, 9, 4), RING2),
                                         ((10239, 11, 3), RING2), ((4777, 20, 4), RING), ((4778, 20, 3), RING2),
-                                        ((4095, 20, 4), PAIR), ((4095, 20, 3), RING), ((1000, 30, 4), PAIR),
+                                        ((4095, 20, 4), SLIDE), ((4095, 20, 3), RING), ((1000, 30, 4), SLIDE),
                                         ((8192, 12, 4), STRIP), ((10240, 5, 3), TWIN), ((11000, 5, 4), TWIN),
                                         ((10241, 9, 3), TWIN), ((12000, 7, 4), TWIN), ((20000, 5, 3), TWIN)],
                          ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
