@@ -1173,11 +1173,12 @@ __device__ __forceinline__ void y_rgb_from_rgba(uint32_t v, uint32_t& y, uint32_
 
 // classify_y<false> with every reference in registers: X (Y space) and its RGB
 // spread xr, L and its spread lrgb; the luma hit's difference is read again from
-// the ring at (i + loff[k]) mod RING (loff[k] = -offset of reference k).
+// the ring at byte (i4 + loff4[k]) mod 4 RING (i4 = 4 i, loff4[k] = -4 offset of
+// reference k).
 __device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32_t L, uint32_t lrgb, uint32_t L2,
                                                  uint32_t L3, uint32_t U, uint32_t UR1, uint32_t UR3, uint32_t UL3,
                                                  uint32_t U2, uint32_t V, uint32_t VR1, uint32_t VL1, uint32_t VL3,
-                                                 uint32_t VR3, const uint32_t* ring, uint32_t i, const uint32_t* loff,
+                                                 uint32_t VR3, const uint32_t* ring, uint32_t i4, const uint32_t* loff4,
                                                  uint32_t cbr, uint32_t csd) {
   // back references k = 1..4 (code.rs:191-206)
   const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
@@ -1203,7 +1204,9 @@ __device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32
     const uint32_t m = min(min(min(min(key[0], key[1]), key[2]), min(min(key[3], key[4]), key[5])),
                            min(min(min(key[6], key[7]), key[8]), min(key[9], key[10])));
     lk = min(m, 11u);
-    lt = xk - ring[(i + loff[m & 15u]) & (CLS_RING - 1)];
+    // loff4[k]: -4 (offset of reference k) mod 4 RING bytes (0 at k = 11)
+    lt = xk - *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ring) +
+                                                  ((i4 + loff4[lk]) & ((CLS_RING - 1) * 4)));
   }
   const uint32_t r = d - K3(3u);   // = xr + 256 - pred per field
   const uint32_t rec_br = (bk << 3) + cbr;
@@ -1218,6 +1221,13 @@ __device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32
   return br ? rec_br : sd ? rec_sd : (l2 || lk < 11u) ? rec_lu : rec_rgb;
 }
 
+// a lane's records past the frame's end are not stored (1..3 of its 4 remain)
+__device__ __noinline__ void store_tail3(uint32_t* p, uint32_t r0, uint32_t r1, uint32_t r2, int n) {
+  p[0] = r0;
+  if (n > 1) p[1] = r1;
+  if (n > 2) p[2] = r2;
+}
+
 template <int WM>   // W mod 4
 __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
   constexpr int RING = CLS_RING;
@@ -1229,10 +1239,20 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
   constexpr uint32_t D2 = (4u - (uint32_t)(2 * WM) % 4u) % 4u;       // row y-2: i - 2W ..
   constexpr uint32_t D3 = (4u - (uint32_t)(3 * WM + 3) % 4u) % 4u;   // row y-3: i - 3W - 3 ..
   constexpr int NB1 = (int)(D1 + 10u + 3u) / 4, NB2 = (int)(D2 + 4u + 3u) / 4, NB3 = (int)(D3 + 10u + 3u) / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[RING + CLS_GUARD];
-  __shared__ uint32_t hs[C0_N + 2 * SX_N];     // slot histogram (nice_rec.hpp)
-  __shared__ uint32_t loff[16];                // luma reference k: -(its offset) mod RING
-  __shared__ uint32_t wfl[2][CLS_THREADS / 64][2];   // [parity][wave]: first coded pixel, last + 1 (tile-relative)
+  // one block of LDS, laid out so that the histogram sits at address 0: its
+  // atomics' base folds into the instruction's 16-bit offset (placed after
+  // the 67 KB ring it cost one VALU add per atomic, three per pixel)
+  struct SlideLds {
+    uint32_t hs[C0_N + 2 * SX_N];               // slot histogram (nice_rec.hpp)
+    uint32_t loff4[16];                         // luma reference k: -4 (its offset) mod 4 RING
+    uint32_t wfl[2][CLS_THREADS / 64][2];       // [parity][wave]: first coded pixel, last + 1 (tile-relative)
+    __attribute__((aligned(16))) uint32_t ring[RING + CLS_GUARD];
+  };
+  __shared__ SlideLds sl;
+  uint32_t* const hs = sl.hs;
+  uint32_t* const loff4 = sl.loff4;
+  uint32_t* const ring = sl.ring;
+  auto& wfl = sl.wfl;
   const uint64_t total_work = (uint64_t)a.n_frames * (a.tile_hi - a.tile_lo);
   const uint64_t w_begin = (uint64_t)blockIdx.x * a.tiles_per_block;
   const uint64_t w_end = min(w_begin + a.tiles_per_block, total_work);
@@ -1244,7 +1264,8 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
   const int64_t N = (int64_t)W * a.H;
   const uint32_t OFF1 = W + 3u + D1, OFF2 = 2u * W + D2, OFF3 = 3u * W + 3u + D3;
   for (uint32_t b = tid; b < C0_N + 2 * SX_N; b += CLS_THREADS) hs[b] = 0;
-  if (tid < 16) loff[tid] = tid < 11 ? (0u - ((uint32_t)lr_rows((int)tid) * W + (uint32_t)lr_px((int)tid))) & RM : 0u;
+  if (tid < 16)
+    loff4[tid] = tid < 11 ? ((0u - ((uint32_t)lr_rows((int)tid) * W + (uint32_t)lr_px((int)tid))) & RM) * 4u : 0u;
   auto flush = [&](uint32_t frame) {
     __syncthreads();
     for (int b = tid; b < N_BINS; b += CLS_THREADS) {
@@ -1373,8 +1394,8 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
         bal[q] = __builtin_amdgcn_ballot_w64(coded);
         const uint32_t rf = classify_win(X[q], XR[q], L, lrgb, L2, L3, w1[q + 3 + D1], w1[q + 4 + D1],
                                          w1[q + 6 + D1], w1[q + D1], w2[q + D2], w3[q + 3 + D3], w3[q + 4 + D3],
-                                         w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, i0 + (uint32_t)q, loff,
-                                         cbr, csd);
+                                         w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, 4u * (i0 + (uint32_t)q),
+                                         loff4, cbr, csd);
         rec[q] = coded ? rf : cunc;
       }
     } else {
@@ -1411,15 +1432,13 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
       if (lane < 8u) a.cmask[(it.tile() + (wave >> 2)) * (ENC_TILE / 32) + 8u * (wave & 3u) + lane] =
           (uint32_t)(bq >> (32u * hw));
     }
-    // records out, histogram
+    // records out (one 16-byte store; a lane with pixels past the frame's end
+    // stores them one by one), histogram
     uint32_t* recs = a.recs + (uint64_t)f * a.rec_stride + (uint64_t)i0;
-    if (4 * (int)tid + 3 < count) {
-      *reinterpret_cast<uint4*>(recs) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (4 * (int)tid + q < count) recs[q] = rec[q];
-    }
+    if (4 * (int)tid + 3 < count)
+      *reinterpret_cast<uint4*>(__builtin_assume_aligned(recs, 16)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+    else if (4 * (int)tid < count)
+      store_tail3(recs, rec[0], rec[1], rec[2], count - 4 * (int)tid);
     if (tid < 256u * (uint32_t)cur) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) slot_hist_add(hs, rec[q]);
