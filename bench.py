@@ -141,9 +141,22 @@ def max_over_ranks(value, dist, device):
 
 
 # timing phase -> the kernels that implement it (first match in the PMC summary)
-PHASE_KERNELS = {"enc_classify": ["enc_classify_pair_m", "enc_classify_pair", "enc_classify_ring", "enc_classify"],
+PHASE_KERNELS = {"enc_classify": ["enc_classify_slide0", "enc_classify_slide1", "enc_classify_slide2",
+                                  "enc_classify_slide3", "enc_classify_pair_m", "enc_classify_pair",
+                                  "enc_classify_ring", "enc_classify"],
                  "enc_tilebits": ["enc_tilebits_hist", "enc_tilebits"],
                  "dec_reconstruct": ["dec_rows_flow", "dec_rows", "dec_rows_wide", "dec_reconstruct"]}
+
+
+def current_profiles():
+    """profiles/CURRENT.json: the counter summaries measured on the committed
+    tree ({"tree": git tree hash, "pmc_traffic": file, "pmc_sq": file, ...}),
+    so the bench never picks up a mid-round file by name order."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "CURRENT.json")) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
 
 
 def load_traffic(phase, frames, path=None):
@@ -151,10 +164,11 @@ def load_traffic(phase, frames, path=None):
     summary (bytes per frame from separate FETCH_SIZE / WRITE_SIZE passes,
     gfx950-corrected; see profiles/README.md), scaled to this launch's frame
     count; None if absent."""
-    if path is None:   # the newest committed summary (profiles/pmc_traffic_rNN*.json)
-        import glob
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_r*.json")))
-        path = cands[-1] if cands else os.path.join(ROOT, "profiles", "pmc_traffic_r03d.json")
+    if path is None:   # the summary profiles/CURRENT.json names
+        name = current_profiles().get("pmc_traffic")
+        if not name:
+            return None, None
+        path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -166,7 +180,9 @@ def load_traffic(phase, frames, path=None):
     return None, None
 
 
-SQ_KERNELS = {"classify": ["nice::enc_classify_pair_m", "nice::enc_classify_pair", "nice::enc_classify_ring"],
+SQ_KERNELS = {"classify": ["nice::enc_classify_slide0", "nice::enc_classify_slide1", "nice::enc_classify_slide2",
+                           "nice::enc_classify_slide3", "nice::enc_classify_pair_m", "nice::enc_classify_pair",
+                           "nice::enc_classify_ring"],
               "pack": ["nice::enc_pack"], "sync": ["nice::dec_sync"], "emit": ["nice::dec_emit"],
               "rundigits": ["nice::enc_rundigits"], "place": ["nice::dec_place"], "rows": ["nice::dec_rows_flow", "nice::dec_rows"]}
 
@@ -176,12 +192,11 @@ def load_sq(px_per_run=32 * 3840 * 2160, path=None):
     share of the hot kernels, from the newest committed SQ counter passes
     (profiles/pmc_sq_rNN*.txt: tools/pmc_kernel.sh, 32 4K frames per
     dispatch); None if absent."""
-    import glob
-    if path is None:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_sq_r*.txt")))
-        if not cands:
+    if path is None:   # the passes profiles/CURRENT.json names
+        name = current_profiles().get("pmc_sq")
+        if not name:
             return None
-        path = cands[-1]
+        path = os.path.join(ROOT, "profiles", name)
     vals = {}
     try:
         with open(path) as fh:
@@ -207,6 +222,8 @@ def load_sq(px_per_run=32 * 3840 * 2160, path=None):
              "valu_per_px": round(d["SQ_INSTS_VALU"] / px_per_run, 3)}
         if "SQ_INSTS_SALU" in d:
             e["salu_per_px"] = round(d["SQ_INSTS_SALU"] / px_per_run, 3)
+        if "SQ_INSTS_LDS" in d:
+            e["lds_per_px"] = round(d["SQ_INSTS_LDS"] / px_per_run, 3)
         if d.get("SQ_ACTIVE_INST_ANY"):
             e["wait_share"] = round(d.get("SQ_WAIT_INST_ANY", 0.0) / d["SQ_ACTIVE_INST_ANY"], 3)
         if d.get("SQ_LDS_IDX_ACTIVE"):

@@ -1362,6 +1362,7 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
     if (fast) {
       // the windows: base = ring index of (wave's first pixel - OFF_r) plus 4 lane
       const uint32_t sw = (uint32_t)start + 256u * wave;
+      const uint32_t i4 = 4u * i0;
       const uint32_t* b0 = ring + ((sw - 4u) & RM) + 4u * lane;
       const uint32_t* b1 = ring + ((sw - OFF1) & RM) + 4u * lane;
       const uint32_t* b2 = ring + ((sw - OFF2) & RM) + 4u * lane;
@@ -1390,12 +1391,13 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
         const uint32_t L2 = q >= 2 ? X[q - 2] : w0[2 + q];
         const uint32_t L3 = q >= 3 ? X[q - 3] : w0[1 + q];
         const uint32_t lrgb = q >= 1 ? XR[q - 1] : rgb_from_y(w0[3]);
-        const bool coded = 4 * (int)tid + q < count && X[q] != L;
-        bal[q] = __builtin_amdgcn_ballot_w64(coded);
         const uint32_t rf = classify_win(X[q], XR[q], L, lrgb, L2, L3, w1[q + 3 + D1], w1[q + 4 + D1],
                                          w1[q + 6 + D1], w1[q + D1], w2[q + D2], w3[q + 3 + D3], w3[q + 4 + D3],
-                                         w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, 4u * (i0 + (uint32_t)q),
+                                         w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, i4 + 4u * (uint32_t)q,
                                          loff4, cbr, csd);
+        // (the flag after the decision: kept across it, it went through a VGPR)
+        const bool coded = 4 * (int)tid + q < count && X[q] != L;
+        bal[q] = __builtin_amdgcn_ballot_w64(coded);
         rec[q] = coded ? rf : cunc;
       }
     } else {
