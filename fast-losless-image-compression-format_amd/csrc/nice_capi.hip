@@ -450,6 +450,7 @@ int nice_encode_batch_dev(nice_ctx* ctx, void* stream, const uint8_t* d_px, uint
                          dim3(std::min<uint32_t>((T + 7) / 8, std::max<uint32_t>(64u, 2048u / n_frames)), n_frames),
                          dim3(256), 0, st, a, ck == CLS_K_SLIDE ? 1 : 0);   // (>= 2048 blocks in all for few, large frames)
     ctx->last_classify = (int)ck;
+    a.cmask_std = (ck != CLS_K_WINDOW && ck != CLS_K_TINY) ? 1u : 0u;   // (enc_pack reads the flags)
     tm.end(st);
     tm.begin(NICE_PH_ENC_TAILRUNS, st);
     if (a.groups > 1) hipLaunchKernelGGL(enc_group_reduce, dim3(a.groups, n_frames), dim3(256), 0, st, a, 0);

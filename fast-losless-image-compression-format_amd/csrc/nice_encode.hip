@@ -1500,6 +1500,10 @@ __global__ __launch_bounds__(256) void enc_rundigits(EncArgs a, int il) {
           x = (x | (x << 3)) & 0x11111111u;
           m |= x << q;
         }
+        // the standard order back in place (enc_pack reads 16 flags per lane
+        // from it); every source word of the tile was read by this wave's
+        // load above
+        a.cmask[((uint64_t)f * T + t) * (ENC_TILE / 32) + k] = m;
       } else {
         m = a.cmask[((uint64_t)f * T + t) * (ENC_TILE / 32) + k];
       }
@@ -2799,7 +2803,7 @@ struct LanePx {
   uint32_t cm;           // coded flags of the lane's pixels
   uint32_t after;        // first coded pixel after the lane (absolute)
   uint32_t s;            // the lane's first pixel (absolute)
-  uint32_t nb, tmax, xany;
+  uint32_t nb, tmax, rmax;   // bits, longest pixel, longest run after a pixel
   __device__ __forceinline__ uint32_t tot(int q) const { return (tot4[q >> 2] >> (8 * (q & 3))) & 0xFFu; }
 };
 
@@ -2836,14 +2840,22 @@ __device__ __forceinline__ void lane_recs(const EncArgs& a, uint32_t f, uint32_t
     for (int q = 0; q < PW_PX; ++q) rec[q] = (p0 + q < count) ? rp[q] : rec2_unc(0);
   }
 }
+// cmw: the tile's coded-flag words in the standard order (enc_rundigits wrote
+// them; 16 bits per lane) when the frame's classify produced them, else null
+// (bands, the window kernels): then the flags come from the records.
 __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab, uint32_t f, uint32_t tt,
-                                           uint32_t next_tile_px, int lane, const uint32_t (&rec)[PW_PX], LanePx& P) {
+                                           uint32_t next_tile_px, int lane, const uint32_t (&rec)[PW_PX], LanePx& P,
+                                           const uint32_t* cmw) {
   const int64_t start = (int64_t)tt * ENC_TILE;
   const int p0 = PW_PX * lane;
   P.rp = a.recs + (uint64_t)f * a.rec_stride + start + p0;
-  P.cm = 0;
+  if (cmw) {   // one load instead of an extract, compare and insert per pixel
+    P.cm = (cmw[lane >> 1] >> (16u * ((uint32_t)lane & 1u))) & 0xFFFFu;
+  } else {
+    P.cm = 0;
 #pragma unroll
-  for (int q = 0; q < PW_PX; ++q) P.cm |= (rec2_coded(rec[q]) ? 1u : 0u) << q;
+    for (int q = 0; q < PW_PX; ++q) P.cm |= (rec2_coded(rec[q]) ? 1u : 0u) << q;
+  }
   // the first coded pixel after the lane: in the next lane with one, else after the tile
   const unsigned long long lanes = __ballot(P.cm != 0u);
   const unsigned long long later = lane < 63 ? lanes >> (lane + 1) : 0ull;
@@ -2854,7 +2866,7 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
   P.after = nl < 64 ? (uint32_t)start + nf : next_tile_px;
   P.nb = 0;
   P.tmax = 0;
-  P.xany = 0;
+  P.rmax = 0;
 #pragma unroll
   for (int q = 0; q < PW_PX; ++q) {
     if ((q & 3) == 0) {
@@ -2865,7 +2877,7 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
     const uint32_t run = lane_run(P, q);
     const uint2 e0 = pt_entry(tab, r, 0), e1 = pt_entry(tab, r, 1), e2 = pt_entry(tab, r, 2);
     const uint2 e3 = tab.rc[rc_index(run)];
-    P.xany |= run > 64u ? 1u << q : 0u;
+    P.rmax = max(P.rmax, run);   // (a per-pixel flag bit cost three VALU)
     const uint32_t t = e0.y + e1.y + e2.y + e3.y;
     uint32_t v = e0.x;   // exact when t <= 32 (shifts stay below 32 then)
     v = (v << (e1.y & 31u)) | e1.x;
@@ -2877,11 +2889,15 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
     P.tmax = max(P.tmax, t);
     P.nb += t;
   }
-  for (uint32_t m = P.xany; m; m &= m - 1u) {   // run digits past a long run's first two (runs of >= 65)
-    for (uint32_t xr = (lane_run(P, __builtin_ctz(m)) - 1u) >> 6; xr;) {
-      P.nb += tab.rc[xr & 7u].y;
-      if (xr < 8) break;
-      xr >>= 3;
+  if (P.rmax > 64u) {   // run digits past a long run's first two (runs of >= 65)
+    for (int q = 0; q < PW_PX; ++q) {
+      const uint32_t run = lane_run(P, q);
+      if (run <= 64u) continue;
+      for (uint32_t xr = (run - 1u) >> 6; xr;) {
+        P.nb += tab.rc[xr & 7u].y;
+        if (xr < 8) break;
+        xr >>= 3;
+      }
     }
   }
 }
@@ -2902,7 +2918,7 @@ __device__ __forceinline__ void lane_emit(const PackTab& tab, const LanePx& P, u
       n -= 32u;
     }
   };
-  if (__all(P.tmax <= 32u && P.xany == 0u)) {
+  if (__all(P.tmax <= 32u && P.rmax <= 64u)) {
     // every pixel of the wave one composed value, no run past 64 pixels
 #pragma unroll
     for (int q = 0; q < PW_PX; ++q) put(P.v[q], P.tot(q));
@@ -2979,7 +2995,8 @@ __global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncAr
     const bool mine = (uint32_t)wid < nsub;   // wave-uniform
     if (mine) {
       lane_recs(a, f, tt0 + wid, lane, rec);
-      lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, rec, P);
+      lane_codes(a, tab, f, tt0 + wid, a.tile_next[(uint64_t)f * T + tt0 + wid], lane, rec, P,
+                 a.cmask_std ? a.cmask + ((uint64_t)f * T + tt0 + wid) * (ENC_TILE / 32) : nullptr);
       x = wave_incl_scan(P.nb);
     }
     if (lane == 63) wsum[wid] = mine ? x : 0u;

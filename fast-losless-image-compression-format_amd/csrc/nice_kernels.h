@@ -32,6 +32,7 @@ struct EncArgs {
   uint32_t* tile_last;       // n_frames * T
   uint32_t* tile_next;       // n_frames * T
   uint32_t* cmask;           // n_frames * T * 32: coded-pixel flags per tile (enc_classify_pair_m); null in band mode
+  uint32_t cmask_std;        // 1: cmask holds every tile's flags in the standard order by enc_pack time
   uint32_t* tbl;             // n_frames * 858: (code << 5) | len for len <= 25
   uint32_t* tbl_code;        // n_frames * 858: code as u32 (serial path)
   uint8_t* tbl_len8;         // n_frames * 858: u8 length
