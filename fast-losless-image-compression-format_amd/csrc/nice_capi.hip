@@ -717,6 +717,13 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // per frame is the better use of the CUs); wider: always, in frame chunks
   bool split = !single_wave && w >= 64 && strips >= 2 && strips <= split_cap &&
                (!use_rows || (uint64_t)n_frames * strips <= split_cap);
+  // rows of up to 8192 pixels (8 waves) take the dataflow kernel on one CU
+  // rather than strips on several (round 6: the strips' cross-CU hand-offs
+  // cost more than the second CU gains); NICE_DEC_SPLIT forces the strips
+  const uint32_t flow_wpr = ((w + 15) / 16 + 63) / 64;
+  if (split && !opt_set(NICE_OPT_DEC_SPLIT) && use_rows && w <= FLOW_MAX_W_HOST && !opt_on(NICE_OPT_DEC_SEG) &&
+      !(opt_set(NICE_OPT_DEC_FLOW) && opt_val(NICE_OPT_DEC_FLOW) <= 0))
+    split = false;
   if (split) {
     const uint32_t sps = (nseg16 + strips - 1) / strips;
     // every strip >= 2 segments (>= 3 pixels: its first and last three) and <= 256 lanes
@@ -728,18 +735,21 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // block per CU); larger batches: one group and a 4-row ring, so two frames
   // share each CU.  NICE_DEC_FLOW=0 takes dec_rows, =k forces k groups (A/B).
   uint32_t flow_k = 2, flow_ring = 8;
-  bool flow = !split && use_rows && !rows8 && w <= 4096;
+  bool flow = !split && use_rows && !rows8 && w <= FLOW_MAX_W_HOST;
   if (n_frames > (uint32_t)std::max(ctx->cus, 1)) { flow_k = 1; flow_ring = 4; }
   if (opt_set(NICE_OPT_DEC_FLOW)) {
     const int v = (int)opt_val(NICE_OPT_DEC_FLOW);
     if (v <= 0) flow = false;
     else flow_k = (uint32_t)v;
   }
-  const uint32_t flow_wpr = ((w + 15) / 16 + 63) / 64;
   if (flow_k * flow_wpr > FLOW_THREADS_HOST / 64) flow_k = FLOW_THREADS_HOST / 64 / flow_wpr;
   if (flow_k > 4 || flow_k < 1) flow = false;   // (stamps of 8 rows)
   if (flow_k > 1) flow_ring = 8;
-  const size_t flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)flow_ring * (w + (w >> 4) + 24) + 4) * 4;   // rows_ring_stride
+  size_t flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)flow_ring * (w + (w >> 4) + 24) + 4) * 4;   // rows_ring_stride
+  if (flow_lds > 160 * 1024 && flow_k == 1 && flow_ring == 8) {   // wide rows: a 4-row ring (one row group)
+    flow_ring = 4;
+    flow_lds = FLOW_CTL_BYTES_HOST + ((size_t)flow_ring * (w + (w >> 4) + 24) + 4) * 4;
+  }
   if (flow_lds > 160 * 1024) flow = false;
   const size_t hand = split ? (size_t)n_frames * h * strips * SPLIT_GRAN_HOST * 8 : 0;
   // per-frame redo flags: the split kernel's, and the dataflow kernel's (a

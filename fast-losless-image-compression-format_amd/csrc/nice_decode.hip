@@ -2431,7 +2431,7 @@ __global__ __launch_bounds__(512) void dec_rows8(DecArgs a) { dec_rows_body<512,
 constexpr uint32_t FLOW_THREADS = 512;
 constexpr uint32_t FLOW_SLOTS = 8;   // stamp slots
 
-constexpr uint32_t FLOW_MAXW = 4;
+constexpr uint32_t FLOW_MAXW = 8;   // waves per row: W <= 8192 (round 6; 4 before)
 constexpr unsigned long long FLOW_TIMEOUT = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
 // a timed-out wait (the workgroup preempted or time-sliced for longer than
 // that) does not fail the frame: it is marked for the barrier kernel

@@ -246,7 +246,8 @@ __global__ void dec_rows(DecArgs a);
 __global__ void dec_rows_wide(DecArgs a);
 __global__ void dec_rows8(DecArgs a);
 __global__ void dec_rows_flow(DecArgs a);   // small batches: rows in flight, LDS stamps (W <= 4096)
-constexpr uint32_t FLOW_THREADS_HOST = 512, FLOW_CTL_BYTES_HOST = 1984;   // == FLOW_THREADS, sizeof(FlowCtl)
+constexpr uint32_t FLOW_THREADS_HOST = 512, FLOW_CTL_BYTES_HOST = 2752;   // == FLOW_THREADS, sizeof(FlowCtl)
+constexpr uint32_t FLOW_MAX_W_HOST = 8192;   // 8 waves of 16-pixel segments per row (FLOW_MAXW)
 __global__ void dec_rows_split(DecArgs a);
 constexpr uint32_t SPLIT_THREADS_HOST = 256;   // == SPLIT_THREADS (nice_decode.hip): lanes per strip
 constexpr uint32_t SPLIT_GRAN_HOST = 8;        // == SPLIT_GRAN

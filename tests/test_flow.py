@@ -9,7 +9,8 @@ two, three and four waves on a row, partial last segments and waves
 (W % 16 in {1, 2}: column W-3 in the second-to-last segment, which can sit in
 the previous wave), every row-group count the kernel takes, and a batch of
 frames: the pixels must equal the input, as with the barrier kernel (dec_rows,
-NICE_DEC_FLOW=0)."""
+NICE_DEC_FLOW=0).  Round 6: rows of 4097..8192 pixels (5..8 waves, one row
+group, 4-row ring) take this kernel too instead of the strip split."""
 import numpy as np
 import pytest
 
@@ -34,7 +35,8 @@ def _decode(nice, s, C):
     return np.frombuffer(got, np.uint8).reshape(-1, C)[:, :3].reshape(-1)
 
 
-@pytest.mark.parametrize("W", [64, 66, 1025, 1026, 1040, 1921, 2050, 3073, 3840, 4096])
+@pytest.mark.parametrize("W", [64, 66, 1025, 1026, 1040, 1921, 2050, 3073, 3840, 4096,
+                               4097, 5000, 6145, 7680, 8192])   # round 6: up to 8 waves per row
 def test_flow_widths(nice, O, W, opts):
     H = 40
     for C in (3, 4):
