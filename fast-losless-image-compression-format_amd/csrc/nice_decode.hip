@@ -1120,18 +1120,31 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_strict_refill(DecArgs a
 // Records of a lane are combined into aligned groups of four and stored with
 // one 16-byte store when the group lies inside the lane's pixel range.
 // ---------------------------------------------------------------------------
-// Record: bits 0..23 the additive constant c (R | G << 8 | B << 16), bits
-// 24..27 the source class: 0 = AVG, 1..3 = the pixel 1..3 back in raster order
-// (a run pixel is class 1 with c = 0), 4..13 = a pixel in a row above, at
-// (rows back, pixels back) = cls_rows / cls_px.
-constexpr uint32_t REC_RUN = 1u << 24;
-// Records written by a decode call carry its tag (1..15) in bits 28..31; a
-// slot without the current tag (stale, or cleared to 0) is a run pixel.  The
-// record buffer is then cleared only when its tags wrap or its layout changes
-// (nice_capi.hip), not prefilled with REC_RUN by every call.
-constexpr uint32_t REC_TAG_SHIFT = 28;
+// Record (round 6): the additive constant c in the row kernels' spread form
+// (R | G << 10 | B << 20: bits 0..7, 10..17, 20..27), bits 28..31 the source
+// class: 0 = AVG, 1..3 = the pixel 1..3 back in raster order (a run pixel is
+// class 1 with c = 0), 4..13 = a pixel in a row above, at (rows back, pixels
+// back) = cls_rows / cls_px.  The record writers (dec_emit, dec_place) spread
+// the constant, so the row kernels' pre-pass -- on the row chain -- only masks
+// it (round 5 kept bytes and spread every pixel there: ~5 VALU per pixel).
+constexpr uint32_t REC_RUN = 1u << 28;
+constexpr uint32_t REC_K = 0xFFu | (0xFFu << 10) | (0xFFu << 20);   // the constant's bits
+// Records written by a decode call carry its tag (1..15) in the gap bits 8..9
+// (tag & 3) and 18..19 (tag >> 2); a slot without the current tag (stale, or
+// cleared to 0) is a run pixel.  The record buffer is then cleared only when
+// its tags wrap or its layout changes (nice_capi.hip), not prefilled with
+// REC_RUN by every call.  The canonical record keeps the tag bits: readers take
+// the class (rec_cls) and the constant (rec_c) only.
+constexpr uint32_t REC_TAG_MASK = (3u << 8) | (3u << 18);
+__device__ __forceinline__ uint32_t rec_tagbits(uint32_t tag) { return ((tag & 3u) << 8) | ((tag >> 2) << 18); }
 __device__ __forceinline__ uint32_t rec_canon(uint32_t r, uint32_t tag) {
-  return (r >> REC_TAG_SHIFT) == tag ? (r & ((1u << REC_TAG_SHIFT) - 1u)) : REC_RUN;
+  return (r & REC_TAG_MASK) == rec_tagbits(tag) ? r : REC_RUN;
+}
+__device__ __forceinline__ uint32_t rec_cls(uint32_t r) { return r >> 28; }
+__device__ __forceinline__ uint32_t rec_c(uint32_t r) { return r & REC_K; }
+// R | G << 8 | B << 16 -> spread (the record writers)
+__device__ __forceinline__ uint32_t rec_spread(uint32_t v) {
+  return (v & 0xFFu) | ((v & 0xFF00u) << 2) | ((v & 0xFF0000u) << 4);
 }
 __host__ __device__ constexpr int cls_rows(int c) {
   return c < 4 ? 0 : c == 4 ? 1 : c == 5 ? 1 : c == 6 ? 2 : c == 7 ? 1 : c <= 10 ? 3 : c == 11 ? 1 : c <= 13 ? 3 : 0;
@@ -1185,19 +1198,19 @@ __device__ __forceinline__ uint32_t make_event_rec(uint64_t W, uint32_t mode, ui
   const int64_t off = (int64_t)(rows * W) + (int64_t)((CLS_PX_PACK >> (3 * cls)) & 7u) - 3;
   const bool bad0 = (isbr && s0 >= 5u) || (islu && s0 >= 11u) || off < 0;
   const uint32_t gl = (s1 - 32u) & 255u;
-  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
+  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 10) | (((s3 - 16u + gl) & 255u) << 20);
   const uint32_t rd = s0 % 7u, t1 = s0 / 7u;
-  const uint32_t c_sd = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
+  const uint32_t c_sd = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 10) | ((((t1 / 7u) - 3u) & 255u) << 20);
   const uint32_t g2 = (s0 - 32u) & 255u;
-  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
-  const uint32_t c_rgb = (s0 & 255u) | ((s1 & 255u) << 8) | ((s2 & 255u) << 16);
-  const uint32_t r = (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 10) | (((s2 - 16u + g2) & 255u) << 20);
+  const uint32_t c_rgb = (s0 & 255u) | ((s1 & 255u) << 10) | ((s2 & 255u) << 20);
+  const uint32_t r = (isbr || islu) ? ((cls << 28) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
   return r | (isl2 ? EV_L2 : 0u) | ((isbr || islu) && bad0 ? EV_BAD : 0u);
 }
 // The reference panics on this pixel at position q: a reference before the
 // image start (code.rs:141-145 offsets) or LUMA2 on the first row (code.rs:583).
 __device__ __forceinline__ bool rec_bad_at(uint32_t ev, uint64_t q, uint64_t W) {
-  const uint32_t cls = (ev >> 24) & 15u;
+  const uint32_t cls = rec_cls(ev);
   const uint64_t rows = (CLS_ROWS_PACK >> (2 * cls)) & 3u;
   const uint64_t off = rows * W + ((CLS_PX_PACK >> (3 * cls)) & 7u) - 3u;   // >= 0 unless EV_BAD
   return (ev & EV_BAD) || ((ev & EV_L2) ? q < W : (cls != 0u && q < off));
@@ -1206,7 +1219,7 @@ __device__ __forceinline__ uint32_t make_record(uint64_t W, uint64_t q, uint32_t
                                                 uint32_t s1, uint32_t s2, uint32_t s3, bool& bad) {
   const uint32_t ev = make_event_rec(W, mode, s0, s1, s2, s3);
   bad = rec_bad_at(ev, q, W);
-  return ev & 0x0FFFFFFFu;
+  return ev & ~(EV_L2 | EV_BAD);
 }
 
 struct RecGroup {
@@ -1363,7 +1376,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
         bool bad;
         const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
         if (bad) { err = true; active = false; continue; }
-        G.put(rec, q0, cur, r | (a.rec_tag << REC_TAG_SHIFT));
+        G.put(rec, q0, cur, r | rec_tagbits(a.rec_tag));
         q = cur + 1;
         closed = false;
       } else {
@@ -1471,22 +1484,22 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
 #endif
   const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0l >= 11u) || off3 < 3u || q + 3u < off3;
   const uint32_t gl = (s1 - 32u) & 255u;
-  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 8) | (((s3 - 16u + gl) & 255u) << 16);
+  const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 10) | (((s3 - 16u + gl) & 255u) << 20);
   const uint32_t c_sd = sdl[min(s0, 342u)];
   const uint32_t g2 = (s0 - 32u) & 255u;
-  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 8) | (((s2 - 16u + g2) & 255u) << 16);
-  uint32_t c_rgb = (s0 & 255u) | (s1 << 8) | (s2 << 16);
+  const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 10) | (((s2 - 16u + g2) & 255u) << 20);
+  uint32_t c_rgb = (s0 & 255u) | (s1 << 10) | (s2 << 20);
   bad = (isbr || islu) ? bad_ref : (isl2 && q < W);
 #ifndef NICE_PLACE_BRANCHY
   // the candidates opaque: otherwise the select chain compiles to a switch of
   // exec-masked branches on the prefix (about 35 scalar instructions and 8
   // branches per event, every prefix present in most waves)
-  uint32_t c_br = (cls << 24) | (islu ? c_lu : 0u);
+  uint32_t c_br = (cls << 28) | (islu ? c_lu : 0u);
   uint32_t c_sd2 = c_sd, c_l22 = c_l2;
   asm volatile("" : "+v"(c_br), "+v"(c_sd2), "+v"(c_l22), "+v"(c_rgb));
   return (isbr || islu) ? c_br : issd ? c_sd2 : isl2 ? c_l22 : c_rgb;
 #else
-  return (isbr || islu) ? ((cls << 24) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
+  return (isbr || islu) ? ((cls << 28) | (islu ? c_lu : 0u)) : issd ? c_sd : isl2 ? c_l2 : c_rgb;
 #endif
 }
 
@@ -1501,7 +1514,7 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
   }
   for (uint32_t i = threadIdx.x; i < 343u; i += blockDim.x) {
     const uint32_t rd = i % 7u, t1 = i / 7u;
-    sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 8) | ((((t1 / 7u) - 3u) & 255u) << 16);
+    sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 10) | ((((t1 / 7u) - 3u) & 255u) << 20);
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
@@ -1589,7 +1602,7 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             if (i + 64u * k >= nev) break;
-            if (i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qb[k]] = r[k] | (a.rec_tag << REC_TAG_SHIFT);
+            if (i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qb[k]] = r[k] | rec_tagbits(a.rec_tag);
           }
           q = base;
           continue;
@@ -1637,7 +1650,7 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool keep = (uint32_t)k < stop_k || ((uint32_t)k == stop_k && lane < stop_lane);
-      if (keep && i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qk[k]] = r[k] | (a.rec_tag << REC_TAG_SHIFT);
+      if (keep && i + 64u * k + lane < nev && !(ev[k] & EV_RUN)) rec[qk[k]] = r[k] | rec_tagbits(a.rec_tag);
     }
     if (stop_k < 4u) {
       if (lane == 0) err = stop_at_n ? (strict && stop_run) : true;
@@ -1723,10 +1736,10 @@ __device__ __forceinline__ int run_segment(const RowCtx& rc, const RecLds& L, co
   for (uint32_t x = x0; x < x_stop; ++x) {
     const uint32_t r = recs[x];
     const uint32_t u = up[x];
-    const bool ref = (r >> 24) != 0;   // run pixels are class 1 (the pixel before) with c = 0
-    const uint32_t c = spread3(r & 0xFFFFFFu);
+    const bool ref = rec_cls(r) != 0;   // run pixels are class 1 (the pixel before) with c = 0
+    const uint32_t c = rec_c(r);
     // reference value (kind REF): recent pixels or a pixel of the ring
-    const int id = (int)((r >> 24) & 15u);
+    const int id = (int)rec_cls(r);
     const int off = (int)L.ref_off32[id];
     int jx = (int)x - L.ref_d[id];
     int jy = (int)y - L.ref_k[id];
@@ -2153,12 +2166,12 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 #pragma unroll
       for (int p = 0; p < S; ++p) {
         const uint32_t r = rec_canon(rn[p] + z, a.rec_tag);
-        const uint32_t cls = r >> 24;                        // 0..13
+        const uint32_t cls = rec_cls(r);                     // 0..13
         const uint2 e = tb[cls];
         uint32_t ad = lb + e.y;
         if (p < 3 || p > S - 4) ad += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
         const uint32_t o = ring[ad + p];
-        const uint32_t c = spread3(r & 0xFFFFFFu);
+        const uint32_t c = rec_c(r);
         // (a VALU mask from a table bit instead of the compare: 4 % slower)
         w[p] = (e.x & 0xF0000000u) | (((cls >= 4u ? o : 0u) + c) & SP_K);
       }
@@ -2171,10 +2184,10 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
 #pragma unroll
         for (int p = 0; p < S; ++p) {
           const uint32_t r = rec_canon(rn[p], a.rec_tag);   // padding: a run record (class 1)
-          const uint32_t cls = r >> 24;
+          const uint32_t cls = rec_cls(r);
           const uint32_t tx = x0 + p + 3u - ((uint32_t)(CLS_PX_PACK >> (3u * cls)) & 7u);
           const bool cur = cls >= 4u && ((CLS_ROWS_PACK >> (2u * cls)) & 3u) == 1u && tx >= W;
-          w[p] = cur ? (W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8)) : w[p];
+          w[p] = cur ? (W_CUR | rec_c(r) | ((tx - W) << 8)) : w[p];
         }
       }
     } else {
@@ -2182,7 +2195,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
     for (int p = 0; p < S; ++p) {
       const uint32_t x = x0 + p;
       const uint32_t r = rec_canon(rn[p] + z, a.rec_tag);
-      const uint32_t cls = r >> 24;                          // 0..13
+      const uint32_t cls = rec_cls(r);                       // 0..13
       const uint32_t cw = cwt[cls];                          // rows | px + 3 << 2 | kind bits
       const uint32_t rows = cw & 3u;
       const int dx = (int)((cw >> 2) & 7u) - 3;
@@ -2195,7 +2208,7 @@ __device__ __forceinline__ void dec_rows_body(const DecArgs& a) {
       // unconditional LDS read (a harmless in-range address for other classes)
       const uint32_t txc = (uint32_t)min(max(tx, 0), (int)W - 1);
       const uint32_t o = ring[__umul24((y - back) & (ROWS_RING - 1), RS) + txc + (txc >> 4)];
-      const uint32_t c = spread3(r & 0xFFFFFFu);
+      const uint32_t c = rec_c(r);
       // kind bits from the class (branch-free: the ternary chain compiled to two
       // nested exec-masked branches per pixel)
       const uint32_t kb = (cw & 0xF0000000u) | (cur ? W_CUR : 0u);
@@ -2627,21 +2640,30 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
 #pragma unroll
     for (int p = 0; p < S; ++p) {
       const uint32_t r = rec_canon(rn[p], a.rec_tag);
-      const uint32_t cls = r >> 24;   // 0..13
+      const uint32_t cls = rec_cls(r);   // 0..13
       const uint2 e = rtab[cls];
       uint32_t idx = lb + e.y + (uint32_t)p;
       if (p < 3 || p > S - 4) idx += (uint32_t)((int)(p + 3u - (e.x & 7u)) >> 4);   // padding word crossed
       ad[p] = cls >= 4u ? idx : ZERO_IDX;
-      wk[p] = (e.x & 0xF0000000u) | spread3(r & 0xFFFFFFu);
+      // kind bits | the constant (already spread by the writers): one bit-field
+      // insert (e.x holds only kind bits 28..31 and dxp3 in bits 0..2, which
+      // the constant's mask covers)
+      uint32_t kw;
+      asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(kw) : "s"(REC_K), "v"(r), "v"(e.x));
+      wk[p] = kw;
     }
-    if (curlane) {   // references past the row end into row y itself (pixels 0..2)
+    // references past the row end into row y itself (pixels 0..2): only the
+    // wave holding the row's last columns (a wave-uniform branch: as a lane
+    // branch the compiler if-converted it into every wave's pre-pass once the
+    // record constant no longer needed spreading here, +2 % reconstruct)
+    if (wave_cur) {
 #pragma unroll
       for (int p = 0; p < S; ++p) {
         const uint32_t r = rec_canon(rn[p], a.rec_tag);
-        const uint32_t cls = r >> 24;
+        const uint32_t cls = rec_cls(r);
         const uint32_t tx = x0 + p + 3u - ((uint32_t)(CLS_PX_PACK >> (3u * cls)) & 7u);
-        const bool cur = cls >= 4u && ((CLS_ROWS_PACK >> (2u * cls)) & 3u) == 1u && tx >= W;
-        wk[p] = cur ? (W_CUR | spread3(r & 0xFFFFFFu) | ((tx - W) << 8)) : wk[p];
+        const bool cur = curlane && cls >= 4u && ((CLS_ROWS_PACK >> (2u * cls)) & 3u) == 1u && tx >= W;
+        wk[p] = cur ? (W_CUR | rec_c(r) | ((tx - W) << 8)) : wk[p];
         ad[p] = cur ? ZERO_IDX : ad[p];
       }
     }
@@ -3081,7 +3103,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
 #pragma unroll
     for (int p = 0; p < S; ++p) {
       const uint32_t r = rec_canon(rn[p], a.rec_tag);
-      const uint32_t cls = r >> 24;
+      const uint32_t cls = rec_cls(r);
       const uint32_t cw = cwt[cls];
       const uint32_t rows = cw & 3u;
       const uint32_t lc3 = xl0 + (uint32_t)p + 6u - ((cw >> 2) & 7u);   // local column + 3 - pixels back
@@ -3090,7 +3112,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void dec_rows_split(DecArgs a) {
       const bool pr = up && rows == 1u && lc3 >= sw + 3u && !hr1;
       const uint32_t lcc = min(lc3, sw + 5u);
       const uint32_t o = ring[__umul24((y - rows) & 3u, RS) + sr_idx(lcc)];
-      const uint32_t c = spread3(r & 0xFFFFFFu);
+      const uint32_t c = rec_c(r);
       const bool cur = pl || pr;
       const uint32_t hslot = pl ? lc3 : (lc3 - sw - 3u);
       const uint32_t kb = (cw & 0xF0000000u) | (cur ? W_CUR : 0u);

@@ -227,9 +227,10 @@ struct DecArgs {
   const uint32_t* unsettled;
 };
 constexpr uint32_t SPLIT_ABORT_ERR = 1u, SPLIT_REDO = 2u;
-// event word: coded pixel = record (bits 0..27) | EV_L2 | EV_BAD; run digit =
-// EV_RUN | pixels (saturated)
-constexpr uint32_t EV_RUN = 1u << 31, EV_BAD = 1u << 29, EV_L2 = 1u << 28;
+// first-pass event of a run digit: EV_RUN | pixels (saturated); a coded
+// pixel's record before its tag: EV_L2 (LUMA2: needs the row above) and EV_BAD
+// in the record's tag bits (make_event_rec, rec_bad_at)
+constexpr uint32_t EV_RUN = 1u << 31, EV_BAD = 1u << 9, EV_L2 = 1u << 8;
 constexpr uint32_t EV_OVERFLOW = 0xFFFFFFFFu, AGREE_NONE = 0xFFFFu;
 
 __global__ void dec_tables(DecArgs a);
