@@ -349,8 +349,17 @@ __global__ __launch_bounds__(256) void dec_tables(DecArgs a) {
 // therefore begin and end at prefix positions: a slice's parse stops at the
 // first prefix at or after its end bit, which is where the next slice starts.
 // ---------------------------------------------------------------------------
-constexpr uint32_t RING_W = 20;        // words per lane ring
-constexpr uint32_t RING_STRIDE = 20;   // 80 bytes: 16-byte aligned rings
+#ifndef NICE_RING_W
+#define NICE_RING_W 20
+#endif
+constexpr uint32_t RING_W = NICE_RING_W;   // words per lane ring (a multiple of 4, >= 12)
+constexpr uint32_t RING_STRIDE = RING_W;   // 16-byte aligned rings
+static_assert(RING_W % 4 == 0 && RING_W >= 12, "ring size");
+#ifdef NICE_PARSE_WPE
+#define PARSE_ATTR __attribute__((amdgpu_waves_per_eu(NICE_PARSE_WPE)))
+#else
+#define PARSE_ATTR
+#endif
 constexpr uint32_t RING_QUADS = RING_W / 4;
 constexpr uint32_t PIXEL_WORDS = 5;    // one pixel event: <= 5 symbols of <= 31 bits
 
@@ -434,11 +443,10 @@ __device__ __noinline__ void ring_fill_slow(uint32_t* dst, const uint8_t* p, uin
 }
 // Wave-cooperative refill: every lane's ring restarts at the word holding its
 // position (rounded down to 16 bytes).  Must be reached by all 64 lanes.
-template <bool FAST = false>
-__device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
-                                          Lane& L) {
+// ws: the (16-byte aligned) stream word each lane's ring restarts at.
+__device__ __forceinline__ void ring_fill_ws(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
+                                             uint32_t ws) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t ws = (uint32_t)(L.pos >> 5) & ~3u;
   const uint64_t full_words = al16 ? (len >> 2) : 0;   // words fully inside the stream
   uint4 v[RING_QUADS];
   uint32_t wq[RING_QUADS];
@@ -465,6 +473,13 @@ __device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uin
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+template <bool FAST = false>
+__device__ __forceinline__ void ring_fill(uint32_t* wring, const uint8_t* p, uint64_t len, bool al16,
+                                          Lane& L) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t ws = (uint32_t)(L.pos >> 5) & ~3u;
+  ring_fill_ws(wring, p, len, al16, ws);
   if constexpr (FAST) {
     L.ws = ws;
   } else {
@@ -586,6 +601,28 @@ __device__ __forceinline__ uint32_t pixel_event_fast(Lane& L, const uint32_t* my
   return pfx;
 }
 
+// pixel_event_fast at ring word o, bit sh of it (dec_sync's relative-position
+// loop); returns the prefix and the event's bit count in tot.
+__device__ __forceinline__ uint32_t pixel_event_fast_at(const uint32_t* my, const LutLds& S, uint32_t fp_pfx,
+                                                        uint32_t o, uint32_t sh, uint32_t& s0, uint32_t& s1,
+                                                        uint32_t& s2, uint32_t& s3, uint32_t& tot) {
+  const uint32_t w0 = my[o], w1 = my[o + 1], w2 = my[o + 2];
+  unsigned long long win = ((((unsigned long long)w0 << 32) | w1) << sh) | (((unsigned long long)w2 << sh) >> 32);
+  tot = 0;
+  const uint32_t pfx = fsym(win, tot, S, fp_pfx);
+  if (pfx < (uint32_t)P_RUN1) {
+    const bool rgb = pfx == (uint32_t)P_RGB, lu = pfx == (uint32_t)P_LUMA, l2 = pfx == (uint32_t)P_LUMA2;
+    const uint4 pp = S.pp[pfx];
+    s0 = fsym(win, tot, S, pp.x);
+    if (rgb || lu || l2) {
+      s1 = fsym(win, tot, S, pp.y);
+      s2 = fsym(win, tot, S, pp.z);
+      if (lu) s3 = fsym(win, tot, S, pp.w);
+    }
+  }
+  return pfx;
+}
+
 // Pixels a prefix accounts for: 1 for a coded pixel; a run digit d contributes
 // d << 3k (k = digits read before it; the reference's u8 shift counter `+= 3`
 // only matters mod 64) plus the run's first pixel on its first digit
@@ -650,7 +687,7 @@ __device__ __forceinline__ uint32_t ev_pack(uint32_t pfx, uint32_t s0, uint32_t 
 // at the fixpoint already and this launch does nothing (the host queues several
 // iterations without waiting for each).
 // `fchanged` (optional): per-frame change flags, for dec_sync_settle.
-__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev,
+__global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs a, uint32_t* changed, const uint32_t* prev,
                                                               uint32_t* fchanged) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
@@ -762,8 +799,106 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_sync(DecArgs a, uint32_
     }
   };
   const bool fast = !a.parse_slow && reinterpret_cast<const DecTables*>(a.tables)[f].fast;
-  if (fast) parse(std::true_type{});
-  else parse(std::false_type{});
+  // Fast parse in 32-bit positions (round 6): r = bits past the word holding
+  // the slice's first bit, so the slice end, stream end, checkpoints and ring
+  // offsets are 32-bit compares and adds instead of 64-bit ones; the loop is
+  // unrolled four times so a kept event goes straight into its slot of the
+  // 16-byte quad (every active lane of the first pass is at the same event
+  // index) instead of through a shift register; a run digit's pixel count is a
+  // 32-bit shift below 2^30.  r counts from the word holding the slice's first
+  // bit or, when the entry lies before the slice (the previous slice's parse
+  // stopped at px > N: speculative garbage), from the entry's word; a wave
+  // with a lane more than 2^30 bits away takes the general symbol-by-symbol
+  // parse, which reads any tables.
+  const unsigned long long B = (active && L.pos < begin ? L.pos : begin) & ~31ull;
+  if (fast && __all(!active || (L.pos >= B && begin + a.chunk_bits - B < (1ull << 30)))) {
+    // the prefix stream's fast parameter (the payload streams' come from S.pp;
+    // a converted copy of SP here put SP in scratch for the general loop)
+    const uint32_t fp_pfx = fast_param(SP.g[PFX_STREAM]);
+    const uint32_t bwl = (uint32_t)(B >> 5);
+    const uint32_t b31 = (uint32_t)(begin - B);   // the slice's first bit
+    const uint32_t rhard = hard > B ? (uint32_t)min(hard - B, (unsigned long long)0xFFFFFFFFu) : 0u;
+    const uint32_t rlim = min(b31 + a.chunk_bits, rhard);
+    uint32_t r = active ? (uint32_t)(L.pos - B) : 0u;
+    uint32_t wsr = (r >> 5) - RING_W;   // ring start word (relative): empty
+    uint32_t nck = b31 + DEC_CK_BITS;   // next checkpoint (relative)
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the current quad of kept events
+    auto step = [&](auto slot_tag, auto keep_tag) -> bool {
+      constexpr int SLOT = decltype(slot_tag)::value;
+      constexpr bool KEEP = decltype(keep_tag)::value;
+      if (active && (r >= rlim || px > N)) active = false;
+      if (active && r >= nck) {
+        const uint32_t cur = (r - b31) | (dk << 20);
+        if (check && k < nvalid_old && (uint32_t)ck_old == cur) {
+          synced = true;
+          active = false;
+        } else {
+          ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
+          if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
+          ++k;
+          nck = k < a.n_ck ? nck + DEC_CK_BITS : 0xFFFFFFFFu;
+          ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
+        }
+      }
+      if (!__any(active)) return false;
+      if (__any(active && (r >> 5) - wsr + 3u > RING_W)) {
+        const uint32_t wsa = (bwl + (r >> 5)) & ~3u;
+        ring_fill_ws(wring, p, len, al16, wsa);
+        wsr = wsa - bwl;
+      }
+      if (active) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, tot;
+        const uint32_t pfx = pixel_event_fast_at(my, S, fp_pfx, (r >> 5) - wsr, r & 31u, s0, s1, s2, s3, tot);
+        r += tot;
+        uint32_t c;
+        if (pfx < (uint32_t)P_RUN1) {
+          dk = 0;
+          c = 1u;
+        } else {
+          const uint32_t sh = (3u * dk) & 63u, d = pfx - (uint32_t)P_RUN1;
+          if (sh < 30u) {
+            c = (d << sh) + (dk == 0 ? 1u : 0u);
+          } else {   // (exact, saturating: only a run of >= 2^30 pixels gets here)
+            const uint64_t c64 = (uint64_t)d << sh;
+            c = c64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c64;
+          }
+          dk = dk >= 64u ? 1u : dk + 1u;
+        }
+        px = sat_add(px, c);
+        if (KEEP && keep) {
+          const uint32_t ev = pfx < (uint32_t)P_RUN1 ? ev_pack(pfx, s0, s1, s2, s3) : EV_RUN | min(c, EV_RUN - 1u);
+          if constexpr (SLOT == 0) q0 = ev;
+          if constexpr (SLOT == 1) q1 = ev;
+          if constexpr (SLOT == 2) q2 = ev;
+          if constexpr (SLOT == 3) {
+            q3 = ev;
+            if (ne < a.ev_cap) *reinterpret_cast<uint4*>(evp + ev_word(ne - 3u)) = make_uint4(q0, q1, q2, q3);
+          }
+          ++ne;
+        }
+      }
+      return true;
+    };
+    if (__any(keep && active)) {   // the first pass: unrolled by the quad
+      for (;;) {
+        if (!step(std::integral_constant<int, 0>{}, std::true_type{})) break;
+        if (!step(std::integral_constant<int, 1>{}, std::true_type{})) break;
+        if (!step(std::integral_constant<int, 2>{}, std::true_type{})) break;
+        if (!step(std::integral_constant<int, 3>{}, std::true_type{})) break;
+      }
+    } else {   // later passes keep nothing (a smaller loop: these launches are short)
+      while (step(std::integral_constant<int, 0>{}, std::false_type{})) {
+      }
+    }
+    L.pos = B + r;
+    // the tail below stores the last (ne & 3) events from ev0..ev2 (newest last)
+    const uint32_t sl = ne & 3u;
+    ev0 = q0;
+    ev1 = sl == 3u ? q1 : q0;
+    ev2 = sl == 3u ? q2 : sl == 2u ? q1 : q0;
+  } else {
+    parse(std::false_type{});   // (any tables; the general parse)
+  }
   if (tstat) {
     const unsigned long long tw = __builtin_amdgcn_s_memtime() - tw0;
     if ((threadIdx.x & 63u) == 0) {
@@ -1261,7 +1396,7 @@ struct RecGroup {
 // not depend on the slice size the sync pass uses.  With the first pass's
 // events kept (a.ev), the lanes take dec_heads' list instead and each stops at
 // its slice's meeting point; dec_place writes the rest.
-__global__ __launch_bounds__(DEC_PARSE_THREADS) void dec_emit(DecArgs a) {
+__global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_emit(DecArgs a) {
   __shared__ LutLds S;
   __shared__ __attribute__((aligned(16))) uint32_t ring[DEC_PARSE_THREADS * RING_STRIDE];
   const uint32_t f = blockIdx.x / a.emit_blocks;

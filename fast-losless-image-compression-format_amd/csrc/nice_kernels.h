@@ -117,7 +117,10 @@ __global__ void enc_classify_twin3(EncArgs a);
 __global__ void enc_classify_twin3_m(EncArgs a);
 constexpr uint32_t CLS_PAIR_MAX_W = 4095;
 // dec_sync / dec_emit block size: one LUT copy per 8 waves (LDS sets occupancy)
-constexpr uint32_t DEC_PARSE_THREADS = 512;
+#ifndef NICE_PARSE_THREADS
+#define NICE_PARSE_THREADS 512
+#endif
+constexpr uint32_t DEC_PARSE_THREADS = NICE_PARSE_THREADS;
 constexpr uint32_t CLS_THREADS_HOST = 512;   // == CLS_THREADS (nice_encode.hip)   // enc_classify_ring: 3W + 3 + 2 tiles fit its 16K-pixel ring
 __global__ void enc_tailruns(EncArgs a);
 __global__ void enc_tables(EncArgs a);
