@@ -2867,6 +2867,20 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
   P.nb = 0;
   P.tmax = 0;
   P.rmax = 0;
+  // each pixel's run-code index, from the last pixel back: the next coded
+  // pixel is carried in a register instead of a bit scan per pixel
+  uint32_t rci[PW_PX];
+  {
+    uint32_t nx = P.after - P.s;   // lane-relative
+#pragma unroll
+    for (int q = PW_PX - 1; q >= 0; --q) {
+      const bool cq = ((P.cm >> q) & 1u) != 0u;
+      const uint32_t run = cq ? nx - (uint32_t)q - 1u : 0u;
+      rci[q] = rc_index(run);
+      P.rmax = max(P.rmax, run);   // (a per-pixel flag bit cost three VALU)
+      nx = cq ? (uint32_t)q : nx;
+    }
+  }
 #pragma unroll
   for (int q = 0; q < PW_PX; ++q) {
     if ((q & 3) == 0) {
@@ -2874,10 +2888,8 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
       __builtin_amdgcn_sched_barrier(0);   // four pixels' lookups in flight at a time (registers)
     }
     const uint32_t r = rec[q];
-    const uint32_t run = lane_run(P, q);
     const uint2 e0 = pt_entry(tab, r, 0), e1 = pt_entry(tab, r, 1), e2 = pt_entry(tab, r, 2);
-    const uint2 e3 = tab.rc[rc_index(run)];
-    P.rmax = max(P.rmax, run);   // (a per-pixel flag bit cost three VALU)
+    const uint2 e3 = tab.rc[rci[q]];
     const uint32_t t = e0.y + e1.y + e2.y + e3.y;
     uint32_t v = e0.x;   // exact when t <= 32 (shifts stay below 32 then)
     v = (v << (e1.y & 31u)) | e1.x;
@@ -2908,13 +2920,16 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
 // neighbouring lanes; the buffer is zero).
 __device__ __forceinline__ void lane_emit(const PackTab& tab, const LanePx& P, uint32_t* bits, uint32_t pos) {
   unsigned long long acc = 0;
-  uint32_t n = pos & 31u, wi = pos >> 5;
+  uint32_t n = pos & 31u;
+  uint32_t* wp = bits + (pos >> 5);
   auto put = [&](uint32_t val, uint32_t len) {   // len <= 32, val < 2^len
     acc = (acc << len) | val;
     n += len;
     if (n >= 32u) {
-      atomicOr(&bits[wi], (uint32_t)(acc >> (n - 32u)));
-      ++wi;
+      // the completed word, acc >> (n - 32), as one funnel shift (32 <= n < 64);
+      // the word pointer steps instead of an index scaled per flush
+      atomicOr(wp, __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, n));
+      ++wp;
       n -= 32u;
     }
   };
@@ -2946,7 +2961,7 @@ __device__ __forceinline__ void lane_emit(const PackTab& tab, const LanePx& P, u
       }
     }
   }
-  if (n) atomicOr(&bits[wi], (uint32_t)(acc << (32u - n)));
+  if (n) atomicOr(wp, (uint32_t)(acc << (32u - n)));
 }
 
 __global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncArgs a) {
