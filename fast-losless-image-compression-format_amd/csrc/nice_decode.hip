@@ -820,7 +820,8 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
     const uint32_t rhard = hard > B ? (uint32_t)min(hard - B, (unsigned long long)0xFFFFFFFFu) : 0u;
     const uint32_t rlim = min(b31 + a.chunk_bits, rhard);
     uint32_t r = active ? (uint32_t)(L.pos - B) : 0u;
-    uint32_t wsr = (r >> 5) - RING_W;   // ring start word (relative): empty
+    uint32_t wsr = 0;    // ring start word (relative)
+    uint32_t rfill = 0;  // refill once r reaches this (ring empty: at once)
     uint32_t nck = b31 + DEC_CK_BITS;   // next checkpoint (relative)
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the current quad of kept events
     auto step = [&](auto slot_tag, auto keep_tag) -> bool {
@@ -840,11 +841,14 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
           ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
         }
       }
-      if (!__any(active)) return false;
-      if (__any(active && (r >> 5) - wsr + 3u > RING_W)) {
+      // (the first pass tests for the wave's end once per quad: a step after
+      // every lane stopped only evaluates masked conditions)
+      if ((!KEEP || SLOT == 0) && !__any(active)) return false;
+      if (__any(active && r >= rfill)) {   // the next event's 3 words would pass the ring's end
         const uint32_t wsa = (bwl + (r >> 5)) & ~3u;
         ring_fill_ws(wring, p, len, al16, wsa);
         wsr = wsa - bwl;
+        rfill = (wsr + RING_W - 2u) << 5;
       }
       if (active) {
         uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, tot;

@@ -2874,11 +2874,13 @@ __device__ __forceinline__ void lane_codes(const EncArgs& a, const PackTab& tab,
     uint32_t nx = P.after - P.s;   // lane-relative
 #pragma unroll
     for (int q = PW_PX - 1; q >= 0; --q) {
-      const bool cq = ((P.cm >> q) & 1u) != 0u;
-      const uint32_t run = cq ? nx - (uint32_t)q - 1u : 0u;
+      const uint32_t cqm = (uint32_t)__builtin_amdgcn_sbfe((int)P.cm, q, 1);   // coded: ~0
+      const uint32_t run = (nx - (uint32_t)q - 1u) & cqm;
       rci[q] = rc_index(run);
       P.rmax = max(P.rmax, run);   // (a per-pixel flag bit cost three VALU)
-      nx = cq ? (uint32_t)q : nx;
+      // one bit insert (the compiler turned the and-or form into a shift,
+      // compare, select and and-or)
+      asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(nx) : "v"(cqm), "I"(q), "v"(nx));
     }
   }
 #pragma unroll
