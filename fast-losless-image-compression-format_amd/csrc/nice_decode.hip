@@ -1478,7 +1478,36 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_emit(DecArgs
   bool closed = (q == N);          // a run completed exactly at N earlier
   bool err = false;
   RecGroup G{~0ull, REC_RUN, REC_RUN, REC_RUN, REC_RUN, 0u};
-  // the loop, instantiated for the fast and the general parse (as dec_sync)
+  // one pixel event read at a prefix position: a record, a run's pixels, or
+  // the end of the lane's work
+  auto handle = [&](bool at_n, uint32_t pfx, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
+    if (at_n) {
+      // a zero digit of the run that reached N: the reference's run loop
+      // (code.rs:665-671) reads it and adds nothing
+      if (dk != 0 && pfx == (uint32_t)P_RUN1) { (void)pixel_count(pfx, dk); return; }
+      // the reference still reads one more prefix (code.rs:660): a run digit
+      // there makes it copy past its buffer
+      err = err || (strict && pfx >= (uint32_t)P_RUN1);
+      active = false;
+      return;
+    }
+    const uint32_t cur = q;
+    const uint32_t c = pixel_count(pfx, dk);
+    if (pfx < (uint32_t)P_RUN1) {
+      bool bad;
+      const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
+      if (bad) { err = true; active = false; return; }
+      G.put(rec, q0, cur, r | rec_tagbits(a.rec_tag));
+      q = cur + 1;
+      closed = false;
+    } else {
+      const unsigned long long qn = (unsigned long long)q + c;
+      if (qn > N) { err = true; active = false; return; }
+      q = (uint32_t)qn;
+      closed = closed || q == N;
+    }
+  };
+  // the general loop (and, before round 6, the fast one: as dec_sync)
   auto emit = [&](auto fast_tag) {
     constexpr bool FAST = decltype(fast_tag)::value;
     if constexpr (FAST) {
@@ -1499,36 +1528,38 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_emit(DecArgs
       uint32_t pfx;
       if constexpr (FAST) pfx = pixel_event_fast(L, my, S, SP, s0, s1, s2, s3);
       else pfx = pixel_event(L, my, S, SP, s0, s1, s2, s3);
-      if (at_n) {
-        // a zero digit of the run that reached N: the reference's run loop
-        // (code.rs:665-671) reads it and adds nothing
-        if (dk != 0 && pfx == (uint32_t)P_RUN1) { (void)pixel_count(pfx, dk); continue; }
-        // the reference still reads one more prefix (code.rs:660): a run digit
-        // there makes it copy past its buffer
-        err = err || (strict && pfx >= (uint32_t)P_RUN1);
-        active = false;
-        continue;
-      }
-      const uint32_t cur = q;
-      const uint32_t c = pixel_count(pfx, dk);
-      if (pfx < (uint32_t)P_RUN1) {
-        bool bad;
-        const uint32_t r = make_record(a.W, cur, pfx, s0, s1, s2, s3, bad);
-        if (bad) { err = true; active = false; continue; }
-        G.put(rec, q0, cur, r | rec_tagbits(a.rec_tag));
-        q = cur + 1;
-        closed = false;
-      } else {
-        const unsigned long long qn = (unsigned long long)q + c;
-        if (qn > N) { err = true; active = false; continue; }
-        q = (uint32_t)qn;
-        closed = closed || q == N;
-      }
+      handle(at_n, pfx, s0, s1, s2, s3);
     }
   };
   const bool fast = !a.parse_slow && reinterpret_cast<const DecTables*>(a.tables)[f].fast;
-  if (fast) emit(std::true_type{});
-  else emit(std::false_type{});
+  // the fast parse in 32-bit positions relative to B, as dec_sync's (round 6)
+  const unsigned long long B = (active && L.pos < begin ? L.pos : begin) & ~31ull;
+  if (fast && __all(!active || (L.pos >= B && end - B < (1ull << 30)))) {
+    const uint32_t fp_pfx = fast_param(SP.g[PFX_STREAM]);
+    const uint32_t bwl = (uint32_t)(B >> 5);
+    const uint32_t rhard = hard > B ? (uint32_t)min(hard - B, (unsigned long long)0xFFFFFFFFu) : 0u;
+    const uint32_t rlim = active ? min((uint32_t)(end - B), rhard) : 0u;
+    uint32_t r = active ? (uint32_t)(L.pos - B) : 0u;
+    uint32_t wsr = 0, rfill = 0;
+    for (;;) {
+      const bool at_n = q == N && (dk == 0 || closed);   // every pixel accounted for
+      if (active && r >= rlim) active = false;
+      if (!__any(active)) break;
+      if (__any(active && r >= rfill)) {
+        const uint32_t wsa = (bwl + (r >> 5)) & ~3u;
+        ring_fill_ws(wring, p, len, al16, wsa);
+        wsr = wsa - bwl;
+        rfill = (wsr + RING_W - 2u) << 5;
+      }
+      if (!active) continue;
+      uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, tot;
+      const uint32_t pfx = pixel_event_fast_at(my, S, fp_pfx, (r >> 5) - wsr, r & 31u, s0, s1, s2, s3, tot);
+      r += tot;
+      handle(at_n, pfx, s0, s1, s2, s3);
+    }
+  } else {
+    emit(std::false_type{});   // (any tables; the general parse)
+  }
   G.flush(rec, q0, q0);   // last group: per-record stores (the next lane may own the rest)
   if (err) set_status(&a.status[f], NICE_E_FORMAT);
 }
