@@ -1673,8 +1673,23 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
 #endif
 }
 
+// SMALL_DIFF index -> record constant (code.rs:230-247): index = rd + 7 gd + 49 bd
+// (each difference + 3), constant = the three differences in spread form
+struct alignas(16) SdlTable {
+  uint32_t v[344];
+};
+constexpr SdlTable make_sdl_table() {
+  SdlTable t{};
+  for (uint32_t i = 0; i < 343u; ++i) {
+    const uint32_t rd = i % 7u, t1 = i / 7u;
+    t.v[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 10) | ((((t1 / 7u) - 3u) & 255u) << 20);
+  }
+  return t;
+}
+__device__ __constant__ SdlTable kSdl = make_sdl_table();
+
 __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
-  __shared__ uint32_t sdl[343];   // SMALL_DIFF index -> constant (code.rs:230-247)
+  __shared__ __attribute__((aligned(16))) uint32_t sdl[344];   // kSdl (code.rs:230-247)
   __shared__ uint2 idt[16];       // reference id -> {class, rows * W + px + 3}
   if (threadIdx.x < 16u) {
     const uint32_t id = threadIdx.x;
@@ -1682,10 +1697,11 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
     idt[id] = make_uint2(cls, (uint32_t)((CLS_ROWS_PACK >> (2u * cls)) & 3u) * a.W +
                                   (uint32_t)((CLS_PX_PACK >> (3u * cls)) & 7u));
   }
-  for (uint32_t i = threadIdx.x; i < 343u; i += blockDim.x) {
-    const uint32_t rd = i % 7u, t1 = i / 7u;
-    sdl[i] = ((rd - 3u) & 255u) | ((((t1 % 7u) - 3u) & 255u) << 10) | ((((t1 / 7u) - 3u) & 255u) << 20);
-  }
+  // copied from a compile-time table: computing the 343 constants in every
+  // block (divisions by 7 and 49) cost ~120 VALU per wave, and dec_place runs
+  // one short-lived block per four slices
+  if (threadIdx.x < 86u)
+    reinterpret_cast<uint4*>(sdl)[threadIdx.x] = reinterpret_cast<const uint4*>(kSdl.v)[threadIdx.x];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   // grid (slices / waves, frames), XCD-aware: consecutive logical blocks are
