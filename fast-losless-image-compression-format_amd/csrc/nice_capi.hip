@@ -672,9 +672,14 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   // slowest lane of a wave re-synchronises, ~1000 bits) cheap relative to the
   // first pass, short ones keep a small batch filling the GPU: aim for about
   // 256 CUs x 8 waves x 64 lanes x 2 slices, as a power of two in [1K, 16K]
+  // (at least 2048 bits from ~48 Mbit of streams up: a 1024-bit slice holds
+  // no checkpoint, so every Jacobi re-parse and dec_emit walk whole slices --
+  // one 4K frame 9.75 -> 9.61 ms, 4 x 4K 10.03 -> 9.85, 8 x 1080p 5.17 ->
+  // 5.11; one 1080p frame, whose 2048-bit slices leave the GPU emptier, 4.92
+  // -> 4.96: kept at 1024, profiles/r06v_ab_slice_min.log)
   uint64_t total_bits = 0;
   for (uint64_t l : lens) total_bits += l * 8 > D ? l * 8 - D : 0;
-  uint32_t cb = DEC_MIN_CHUNK_BITS;
+  uint32_t cb = total_bits >= (48ull << 20) ? 2 * DEC_MIN_CHUNK_BITS : DEC_MIN_CHUNK_BITS;
   while (cb < DEC_MAX_CHUNK_BITS && total_bits / (2ull * cb) > 256ull * 8 * 64 * 2) cb *= 2;
   if (opt_set(NICE_OPT_DEC_SLICE_BITS)) {   // tests: force a slice size
     const uint32_t v = (uint32_t)opt_val(NICE_OPT_DEC_SLICE_BITS);
