@@ -2009,8 +2009,14 @@ __global__ __launch_bounds__(TR_THREADS) void enc_tailruns(EncArgs a) {
 __global__ __launch_bounds__(64) void enc_tables(EncArgs a) {
   __shared__ HeapLds h;
   __shared__ uint32_t counts[MAX_ALPHABET];
-  const uint32_t f = blockIdx.x / N_STREAMS;
-  const int s = blockIdx.x % N_STREAMS;
+  // stream-major, largest alphabets first (343, 256, 64, 64, 32 x 3, 13, 11,
+  // 11 symbols): the long heap replays start in the first wave of blocks
+  // instead of behind the short ones (a batch's blocks do not all fit at once)
+  const uint32_t nf = gridDim.x / N_STREAMS;
+  constexpr uint64_t ORDER = 5ull | 0ull << 4 | 2ull << 8 | 6ull << 12 | 3ull << 16 | 7ull << 20 | 8ull << 24 |
+                             1ull << 28 | 4ull << 32 | 9ull << 36;
+  const uint32_t f = blockIdx.x % nf;
+  const int s = (int)((ORDER >> (4u * (blockIdx.x / nf))) & 15u);
   const int n = stream_size(s);
   const int sb = stream_base(s);
   const int lane = threadIdx.x;
