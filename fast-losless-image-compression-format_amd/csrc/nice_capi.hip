@@ -686,7 +686,13 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
     if (v >= DEC_MIN_CHUNK_BITS && v <= DEC_MAX_CHUNK_BITS && (v & (v - 1)) == 0) cb = v;
   }
   const uint32_t max_chunks = max_len * 8 > D ? (uint32_t)((max_len * 8 - D + cb - 1) / cb) : 1;
-  const uint32_t n_ck = cb / DEC_CK_BITS - 1;
+  // checkpoints every 512 bits in slices up to 4K bits (small batches: the
+  // re-parses and dec_emit's heads stop at the first meeting point, half as far
+  // in: one 4K frame 9.59 -> 9.52 ms, 64 x 1080p 6.13 -> 6.07), every 1024 from
+  // 8K bits up (512 x 4K: sync 12.0 -> 12.6 ms at 512, more checkpoint stores
+  // than the shorter heads save; profiles/r06x_ab_ck_bits.log)
+  const uint32_t ck_bits = cb <= 4096u ? DEC_CK_BITS_SMALL : DEC_CK_BITS;
+  const uint32_t n_ck = cb / ck_bits - 1;
   const RecGeom g = rec_geom(w);
   // multi-wave row kernel for 64 <= W <= 16384 (one lane per 16-pixel segment),
   // single-wave kernel otherwise
@@ -801,6 +807,7 @@ int nice::decode_batch_impl(nice_ctx* ctx, void* stream, const uint8_t* d_stream
   a.max_chunks = max_chunks;
   a.chunk_bits = cb;
   a.n_ck = n_ck;
+  a.ck_bits = ck_bits;
   a.emit_blocks = (uint32_t)(((uint64_t)max_chunks * (cb / DEC_EMIT_BITS) + DEC_PARSE_THREADS - 1) / DEC_PARSE_THREADS);
   a.chunk_blocks = (max_chunks + DEC_PARSE_THREADS - 1) / DEC_PARSE_THREADS;
   a.chunk_px = (unsigned long long*)(base + L.o_cpx);

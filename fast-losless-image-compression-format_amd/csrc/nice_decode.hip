@@ -736,7 +736,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
   L.ws = (uint32_t)(L.pos >> 5) - RING_W;   // (fast path) empty as well
   uint32_t dk = (uint32_t)(e >> 44) & 127u;
   uint32_t px = 0, k = 0;
-  unsigned long long next_ck = begin + DEC_CK_BITS;
+  unsigned long long next_ck = begin + a.ck_bits;
   unsigned long long ck_old = (check && nvalid_old > 0) ? ck[0] : ~0ull;
   bool active = need, synced = false;
   // diagnostics (builds with -DNICE_SYNC_CYCLES and NICE_DEC_STATS=1, first
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
           ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
           if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
           ++k;
-          next_ck = k < a.n_ck ? next_ck + DEC_CK_BITS : ~0ull;
+          next_ck = k < a.n_ck ? next_ck + a.ck_bits : ~0ull;
           ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
         }
       }
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
     uint32_t r = active ? (uint32_t)(L.pos - B) : 0u;
     uint32_t wsr = 0;    // ring start word (relative)
     uint32_t rfill = 0;  // refill once r reaches this (ring empty: at once)
-    uint32_t nck = b31 + DEC_CK_BITS;   // next checkpoint (relative)
+    uint32_t nck = b31 + a.ck_bits;   // next checkpoint (relative)
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the current quad of kept events
     auto step = [&](auto slot_tag, auto keep_tag) -> bool {
       constexpr int SLOT = decltype(slot_tag)::value;
@@ -837,7 +837,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_sync(DecArgs
           ck[(uint64_t)k * a.max_chunks] = cur | ((unsigned long long)px << 32);
           if (keep) evck[(uint64_t)k * a.max_chunks] = ne;
           ++k;
-          nck = k < a.n_ck ? nck + DEC_CK_BITS : 0xFFFFFFFFu;
+          nck = k < a.n_ck ? nck + a.ck_bits : 0xFFFFFFFFu;
           ck_old = (check && k < nvalid_old) ? ck[(uint64_t)k * a.max_chunks] : ~0ull;
         }
       }
@@ -1395,7 +1395,7 @@ struct RecGroup {
 };
 
 // Lanes take sub-slices of DEC_EMIT_BITS: sub-slice s of slice j starts at the
-// converged parse's checkpoint (s * DEC_EMIT_BITS / DEC_CK_BITS - 1) -- a prefix
+// converged parse's checkpoint (s * DEC_EMIT_BITS / a.ck_bits - 1) -- a prefix
 // position with its run digits and pixel count -- so emission parallelism does
 // not depend on the slice size the sync pass uses.  With the first pass's
 // events kept (a.ev), the lanes take dec_heads' list instead and each stops at
@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(DEC_PARSE_THREADS) PARSE_ATTR void dec_emit(DecArgs
     q64 = a.chunk_start[base + j];   // pixels accounted before this slice
     const uint32_t nvalid = (uint32_t)(a.last[base + j] >> 56);
     const unsigned long long* ck = a.ck + (uint64_t)f * a.n_ck * a.max_chunks + j;
-    const uint32_t step = DEC_EMIT_BITS / DEC_CK_BITS;
+    const uint32_t step = DEC_EMIT_BITS / a.ck_bits;
     if (sub == 0) {
       e = j == 0 ? 0ull : a.entry[base + j];
     } else {
@@ -1579,7 +1579,7 @@ __global__ __launch_bounds__(1024) void dec_heads(DecArgs a) {
   }
   const uint32_t nc = n_chunks(a.stream_len[f], a.data_start[f], a.chunk_bits);
   const uint64_t base = (uint64_t)f * a.max_chunks;
-  const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS, step = DEC_EMIT_BITS / DEC_CK_BITS;
+  const uint32_t subs = a.chunk_bits / DEC_EMIT_BITS, step = DEC_EMIT_BITS / a.ck_bits;
   const uint32_t per = (nc + 1023) / 1024;
   const uint32_t c0 = min(threadIdx.x * per, nc), c1 = min(c0 + per, nc);
   auto nsub = [&](uint32_t j) -> uint32_t {

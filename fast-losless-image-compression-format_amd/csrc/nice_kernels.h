@@ -164,8 +164,10 @@ __global__ void enc_pack_long(EncArgs a, int phase);
 
 namespace nice {
 
-constexpr uint32_t DEC_CK_BITS = 1024;      // sync checkpoint spacing inside a chunk (one per emit sub-slice;
-                                            // 128: +30 % dec_sync -- scattered stores)
+// sync checkpoint spacing inside a slice (DecArgs::ck_bits, chosen per call:
+// at most one emit sub-slice; 128: +30 % dec_sync -- scattered stores)
+constexpr uint32_t DEC_CK_BITS = 1024;      // slices of 8K bits and more (the bench's 512 x 4K)
+constexpr uint32_t DEC_CK_BITS_SMALL = 512;  // shorter slices (small batches)
 constexpr uint32_t DEC_MIN_CHUNK_BITS = 1024;   // speculative-parse slice: a power of two
 constexpr uint32_t DEC_MAX_CHUNK_BITS = 16384;  // chosen per call (nice_capi.hip)
 constexpr uint32_t DEC_PLACE_WAVES = 4;          // dec_place: one wave per slice (2 or 8 per block: slower; several slices per wave, their bookkeeping loads batched: slower too)
@@ -188,7 +190,8 @@ struct DecArgs {
   unsigned long long* entry;          // n_frames * max_chunks packed entry states
   unsigned long long* last;           // n_frames * max_chunks entry of the last parse
   unsigned long long* ck;             // n_frames * n_ck * max_chunks checkpoints
-  uint32_t chunk_bits, n_ck;          // slice size; checkpoints per slice (chunk_bits / DEC_CK_BITS - 1)
+  uint32_t chunk_bits, n_ck;          // slice size; checkpoints per slice (chunk_bits / ck_bits - 1)
+  uint32_t ck_bits;                   // checkpoint spacing (DEC_CK_BITS or DEC_CK_BITS_SMALL)
   uint32_t emit_blocks;               // per frame: ceil(max_chunks * chunk_bits / DEC_EMIT_BITS / 256)
   unsigned long long* chunk_px;       // n_frames * max_chunks
   unsigned long long* chunk_start;    // n_frames * max_chunks
