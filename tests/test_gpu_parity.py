@@ -231,10 +231,12 @@ def test_config3_batch_64x1080p(nice, O):
     assert torch.equal(got, px.view(n, -1, 4)[:, :, :3])
 
 
-@pytest.mark.parametrize("bits", [2048, 16384])
+@pytest.mark.parametrize("bits", [1024, 2048, 4096, 8192, 16384])
 def test_decode_long_slices(nice, O, bits, opts):
-    """Long parse slices: emission runs from checkpoint sub-slices (the default
-    picks them only for large batches)."""
+    """Every parse slice size: emission runs from checkpoint sub-slices (the
+    default picks long slices only for large batches); checkpoints every 512
+    bits up to 4096-bit slices (1024-bit slices hold one), every 1024 from 8192
+    (round 6)."""
     opts.setenv("NICE_DEC_SLICE_BITS", str(bits))
     for name, px, w, h, c in CASES:
         if name not in ("syn512x4", "syn1920x1080x4", "stripes700x300x3", "noise300x200x3"):
