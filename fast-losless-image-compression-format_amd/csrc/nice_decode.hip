@@ -2856,6 +2856,12 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     FLOW_T(0)
     // ---- wait for the rows above
     if (y > 0 && !flow_wait(C, C.fin[(y - 1u) & (FLOW_SLOTS - 1u)], depmask, y)) { ok = false; break; }
+    // wave priorities (round 6): the row's pass once the rows above are in
+    // before the waves still decoding records or storing the raster, and the
+    // fix-up chain -- the row's serial path -- before both (512 x 4K
+    // reconstruct 15.54 -> 14.48 ms, one 4K frame 8.43 -> 7.92;
+    // profiles/r06ze_ab_flow_prio.log, r06zf_ab_flow_prio2.log)
+    __builtin_amdgcn_s_setprio(1);
     FLOW_T(1)
     // ---- pre-pass, part 2: reference values, the row above, the entry
     uint32_t wv[S], prev[S];
@@ -2904,6 +2910,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
     pub_tail();
     FLOW_T(3)
     // ---- fix-up rounds inside the wave
+    __builtin_amdgcn_s_setprio(2);
     bool cur_done = !wave_cur;
     unsigned long long t0 = 0;
     for (uint32_t n = 0;; ++n) {
@@ -2984,6 +2991,7 @@ __global__ __launch_bounds__(FLOW_THREADS) void dec_rows_flow(DecArgs a) {
         ring[((y + 1u) & RM) * RS + lane - 4] = ring[rs * RS + col + (col >> 4)];
     }
     if (lane == 0) flow_publish(&C.fin[s][w], y + 1u);
+    __builtin_amdgcn_s_setprio(0);
     FLOW_T(5)
     // ---- off the critical path: the next row's records, the raster
     if (y + K < H) load_recs(y + K);

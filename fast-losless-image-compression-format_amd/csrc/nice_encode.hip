@@ -3063,9 +3063,13 @@ __global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncAr
     if (!over && mine && P.nb) lane_emit(tab, P, bits, wbase + x - P.nb);
     PROF_MARK(2);
     if (wid == 0 && lookback_mode) {
+      // the look-back first: the groups behind wait on its published prefix
+      // (pack 8.12 -> 8.04 ms per 512 frames, profiles/r06zg_ab_prio.log)
+      __builtin_amdgcn_s_setprio(3);
       const unsigned long long off = lookback(a.status, f * ng + g, g, a.band ? a.band_bit0 : a.seed_bit[f], gbits, lane,
                                               agg_out);
       if (lane == 0) s_off = off;
+      __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
     PROF_MARK(3);
