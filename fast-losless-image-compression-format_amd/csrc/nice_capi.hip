@@ -509,11 +509,13 @@ struct DecLayout {
 // queued iterations', the settle's, the last iteration's.
 constexpr uint32_t kSyncQueuedMax = 16, kSyncFlags = kSyncQueuedMax + 2;
 constexpr uint32_t kSettledFlag = kSyncQueuedMax, kFinalFlag = kSyncQueuedMax + 1;
-// 16: a single 4K SYN-v1 frame needs 5 (with 4 it falls to the serial
-// settle: 3.3 s); each early-exiting launch past the fixpoint costs ~5 us
-// (one 4K frame: resync 0.29 -> 0.34 ms for 8 -> 16, profiles/r05zq3_ab_syncq.log)
+// 8: a single 4K SYN-v1 frame needs 5; round 5 queued 16 to stay clear of its
+// one-lane settle (3.3 s when 4 were queued), but the round-6 parallel settle
+// finishes a frame a few iterations short in ~10 ms, and each early-exiting
+// launch past the fixpoint costs ~5 us (one 4K frame: resync 0.234 -> 0.186
+// ms for 16 -> 8, 512 frames 1.41 -> 1.36; profiles/r06zm_syncq.log)
 #ifndef NICE_SYNC_QUEUED
-#define NICE_SYNC_QUEUED 16
+#define NICE_SYNC_QUEUED 8
 #endif
 constexpr uint32_t kSyncQueued = NICE_SYNC_QUEUED;
 static_assert(kSyncQueued >= 1 && kSyncQueued <= kSyncQueuedMax, "queued sync iterations");
