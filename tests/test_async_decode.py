@@ -109,7 +109,7 @@ def _time_decode(nice, s, runs=3):
 
 def test_settle_slow_sync_stream(nice, O, opts, capfd):
     """a stream that needs more Jacobi iterations than are
-    queued (16).  tests/crafted_streams.make_slow_sync: zero-residual RGB
+    queued (8).  tests/crafted_streams.make_slow_sync: zero-residual RGB
     pixels are 25 zero bits, so a parse that starts at the wrong bit stays
     there until a rare SMALL_DIFF pixel moves it (re-synchronisation after
     ~7 K bits on average, ~34 K at worst: ~35 iterations of 1 K-bit slices).
@@ -128,7 +128,8 @@ def test_settle_slow_sync_stream(nice, O, opts, capfd):
     err = capfd.readouterr().err
     line = [l for l in err.splitlines() if "sync iterations that changed an entry" in l][-1]
     flags = [int(x) for x in line.split(":")[1].split("(")[0].split()]
-    assert flags[15] == 1 and flags[16] == 1 and flags[17] == 0, line   # 16th queued moved; settled; final still
+    queued = int(line.split("(queued")[1].split(",")[0])
+    assert flags[queued - 1] == 1 and flags[16] == 1 and flags[17] == 0, line   # last queued moved; settled; final still
     opts.delenv("NICE_DEC_STATS")
     t_slow, px = _time_decode(nice, s)
     assert np.array_equal(px.reshape(-1), ref)
