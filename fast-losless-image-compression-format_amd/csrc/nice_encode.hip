@@ -1179,7 +1179,7 @@ __device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32
                                                  uint32_t L3, uint32_t U, uint32_t UR1, uint32_t UR3, uint32_t UL3,
                                                  uint32_t U2, uint32_t V, uint32_t VR1, uint32_t VL1, uint32_t VL3,
                                                  uint32_t VR3, const uint32_t* ring, uint32_t i4, const uint32_t* loff4,
-                                                 uint32_t cbr, uint32_t csd) {
+                                                 uint32_t cbr, uint32_t csd, uint32_t pq) {
   // back references k = 1..4 (code.rs:191-206)
   const bool e1 = U == X, e2 = UR1 == X, e3 = L2 == X, e4 = U2 == X;
   const bool br = e1 | e2 | e3 | e4;
@@ -1197,6 +1197,14 @@ __device__ __forceinline__ uint32_t classify_win(uint32_t X, uint32_t xr, uint32
   // luma, 11 references, first hit wins (code.rs:293-339): min-key search
   uint32_t lk = 11u, lt = 0u;
   if (__builtin_amdgcn_ballot_w64(!br && !sd && !l2) != 0ull) {
+    // a wave that takes the luma search issues first until its block's next
+    // barrier (the block waits on its slowest wave), the more so the later in
+    // the lane's four pixels it needs it (pq: 1, 1, 2, 3): classify 15.22 ->
+    // 14.12 ms per 512 frames (profiles/r06zp_ab_cls_prio.log,
+    // r06zq_ab_cls_prio_modes.log; by the count of searches so far: 14.35)
+    if (pq >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (pq == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(1);
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
     uint32_t key[11];
 #pragma unroll
@@ -1355,6 +1363,7 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
       fetch(nx, nti);
     }
     __syncthreads();
+    __builtin_amdgcn_s_setprio(0);   // (raised by classify_win's luma search)
     if (prev_cur) combine();
     const bool fast = start >= 3 * (int64_t)W + 3;   // block-uniform
     uint32_t rec[4];
@@ -1391,10 +1400,11 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
         const uint32_t L2 = q >= 2 ? X[q - 2] : w0[2 + q];
         const uint32_t L3 = q >= 3 ? X[q - 3] : w0[1 + q];
         const uint32_t lrgb = q >= 1 ? XR[q - 1] : rgb_from_y(w0[3]);
+        const uint32_t pq = q == 3 ? 3u : q == 2 ? 2u : 1u;   // (compile-time after unrolling)
         const uint32_t rf = classify_win(X[q], XR[q], L, lrgb, L2, L3, w1[q + 3 + D1], w1[q + 4 + D1],
                                          w1[q + 6 + D1], w1[q + D1], w2[q + D2], w3[q + 3 + D3], w3[q + 4 + D3],
                                          w3[q + 2 + D3], w3[q + D3], w3[q + 6 + D3], ring, i4 + 4u * (uint32_t)q,
-                                         loff4, cbr, csd);
+                                         loff4, cbr, csd, pq);
         // (the flag after the decision: kept across it, it went through a VGPR)
         const bool coded = 4 * (int)tid + q < count && X[q] != L;
         bal[q] = __builtin_amdgcn_ballot_w64(coded);
