@@ -592,6 +592,9 @@ __device__ __forceinline__ uint32_t classify_y(const uint32_t* b0, const uint32_
   // pixel -- was 6 % slower at 512 frames: whole waves often skip it)
   const bool need_luma = __builtin_amdgcn_ballot_w64(!br && !sd && !l2) != 0ull;
   if (need_luma) {
+    // the wave issues first until its block's next tile barrier (as in the
+    // slide kernel's classify_win: the block waits on its slowest wave)
+    if constexpr (!HEAD) __builtin_amdgcn_s_setprio(1);
     const uint32_t refs[11] = {L, U, UR1, UR3, L3, VR1, V, VL1, UL3, VL3, VR3};
     if constexpr (HEAD) {
 #pragma unroll
@@ -785,6 +788,7 @@ __device__ __forceinline__ void enc_classify_ring_body(const EncArgs& a) {
     if (w + 2 < w_end) fetch(nx, pf);
     nx.step(1);
     __syncthreads();
+    __builtin_amdgcn_s_setprio(0);   // (raised by classify_y's luma search)
     // coded flags -> tile bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
     unsigned long long wbal[CLS_PPT];   // coded flags of the wave's 64 pixels per q
@@ -1012,6 +1016,7 @@ __device__ __forceinline__ void enc_classify_pair_body(const EncArgs& a) {
       fetch(nx, nti);
     }
     __syncthreads();
+    __builtin_amdgcn_s_setprio(0);   // (raised by classify_y's luma search)
     // coded flags -> bitmask (a pixel is coded iff i == 0 or Y(i) != Y(i-1))
     uint32_t coded_bits = 0;
     unsigned long long wbal[PQ];

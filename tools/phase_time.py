@@ -1,5 +1,6 @@
 """Diagnostic: per-phase HIP-event times of encode + decode for a batch of F
-RGBA SYN-v1 frames (F=1: single-frame latency).  Usage: phase_time.py F [reps [W H]]"""
+RGBA SYN-v1 frames (F=1: single-frame latency).  Usage: phase_time.py F [reps [W H [C]]]
+(C = 3: RGB input frames, decoded to RGB)"""
 import ctypes, importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -12,12 +13,13 @@ F = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 W = int(sys.argv[3]) if len(sys.argv) > 4 else 3840
 H = int(sys.argv[4]) if len(sys.argv) > 4 else 2160
+C = int(sys.argv[5]) if len(sys.argv) > 5 else 4
 dev = torch.device("cuda", 0)
-px = bench.syn_frames(torch, F, W, H, 1, dev)
+px = bench.syn_frames(torch, F, W, H, 1, dev, C)
 stride = (nice.encode_bound(W, H) + 255) // 256 * 256
 st = torch.empty((F, stride), dtype=torch.uint8, device=dev)
 ln = torch.zeros(F, dtype=torch.int64, device=dev)
-dec = torch.empty((F, W * H * 4), dtype=torch.uint8, device=dev)
+dec = torch.empty((F, W * H * C), dtype=torch.uint8, device=dev)
 status = torch.zeros(F, dtype=torch.int32, device=dev)
 L = nice.lib()
 L.nice_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -25,14 +27,14 @@ L.nice_ctx_read_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_doub
 L.nice_phase_name.restype = ctypes.c_char_p
 ctx = nice._ctx(0)
 for _ in range(2):
-    nice.encode_batch(px, W, H, 4, st, ln)
-    nice.decode_batch(st, ln, W, H, 4, dec, status)
+    nice.encode_batch(px, W, H, C, st, ln)
+    nice.decode_batch(st, ln, W, H, C, dec, status)
 torch.cuda.synchronize()
 assert int(status.abs().sum()) == 0
 if not os.environ.get("NICE_PT_NOCHECK"):   # (timing-only experiment builds)
     assert torch.equal(dec.reshape(F, -1), px.reshape(F, -1)), "decoded frames differ from the input"
-for what, fn in [("encode", lambda: nice.encode_batch(px, W, H, 4, st, ln)),
-                 ("decode", lambda: nice.decode_batch(st, ln, W, H, 4, dec, status))]:
+for what, fn in [("encode", lambda: nice.encode_batch(px, W, H, C, st, ln)),
+                 ("decode", lambda: nice.decode_batch(st, ln, W, H, C, dec, status))]:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
