@@ -1655,14 +1655,9 @@ __device__ __forceinline__ uint32_t place_record(uint32_t ev, uint32_t q, uint32
   const bool bad_ref = (isbr && s0 >= 5u) || (islu && s0l >= 11u) || off3 < 3u || q + 3u < off3;
   const uint32_t gl = (s1 - 32u) & 255u;
   const uint32_t c_lu = ((s2 - 16u + gl) & 255u) | (gl << 10) | (((s3 - 16u + gl) & 255u) << 20);
-#ifndef NICE_PLACE_SDL_ARITH
+  // (a conflict-free form by two reciprocal multiplies instead of this
+  // gather measured the same: r06zr_ab_place_sdl_arith.log)
   const uint32_t c_sd = sdl[min(s0, 342u)];
-#else
-  // index = rd + 7 gd + 49 bd by two reciprocal multiplies (exact for s <= 342):
-  // no LDS gather (random indices, a third of dec_place's LDS cycles conflicted)
-  const uint32_t ss = min(s0, 342u), t7 = (ss * 9363u) >> 16, bd = (t7 * 9363u) >> 16;
-  const uint32_t c_sd = (((ss - 7u * t7) | ((t7 - 7u * bd) << 10) | (bd << 20)) + 253u * 0x100401u) & (255u * 0x100401u);
-#endif
   const uint32_t g2 = (s0 - 32u) & 255u;
   const uint32_t c_l2 = ((s1 - 16u + g2) & 255u) | (g2 << 10) | (((s2 - 16u + g2) & 255u) << 20);
   uint32_t c_rgb = (s0 & 255u) | (s1 << 10) | (s2 << 20);
