@@ -1458,6 +1458,8 @@ __device__ __forceinline__ void enc_classify_slide_body(const EncArgs& a) {
       store_tail3(recs, rec[0], rec[1], rec[2], count - 4 * (int)tid);
     if (tid < 256u * (uint32_t)cur) {
 #pragma unroll
+      // (same-address adds cost nothing extra: every lane on its own zero
+      // slots instead measured slower, 14.07 -> 14.74 ms, r06zt_hist_probe.log)
       for (int q = 0; q < 4; ++q) slot_hist_add(hs, rec[q]);
     }
     prev_tile = it.tile();

@@ -26,15 +26,17 @@ L.nice_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 L.nice_ctx_read_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
 L.nice_phase_name.restype = ctypes.c_char_p
 ctx = nice._ctx(0)
+ENC_ONLY = bool(os.environ.get("NICE_PT_ENC_ONLY"))   # (probe builds whose streams are not valid)
 for _ in range(2):
     nice.encode_batch(px, W, H, C, st, ln)
-    nice.decode_batch(st, ln, W, H, C, dec, status)
+    if not ENC_ONLY:
+        nice.decode_batch(st, ln, W, H, C, dec, status)
 torch.cuda.synchronize()
 assert int(status.abs().sum()) == 0
-if not os.environ.get("NICE_PT_NOCHECK"):   # (timing-only experiment builds)
+if not os.environ.get("NICE_PT_NOCHECK") and not ENC_ONLY:   # (timing-only experiment builds)
     assert torch.equal(dec.reshape(F, -1), px.reshape(F, -1)), "decoded frames differ from the input"
 for what, fn in [("encode", lambda: nice.encode_batch(px, W, H, C, st, ln)),
-                 ("decode", lambda: nice.decode_batch(st, ln, W, H, C, dec, status))]:
+                 ("decode", lambda: nice.decode_batch(st, ln, W, H, C, dec, status))][:1 if ENC_ONLY else 2]:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
