@@ -1727,6 +1727,8 @@ __global__ __launch_bounds__(64 * DEC_PLACE_WAVES) void dec_place(DecArgs a) {
     atomicAdd(&a.stats[50 + b], 1ull);
   }
   if (ag == AGREE_NONE || nev == EV_OVERFLOW || ag > nvalid) return;   // dec_emit parsed it all
+  // (the bookkeeping loads issued together, the first checkpoint taken as
+  // the meeting point before `agree` is in: no faster, r06zv_ab_pack_place.log)
   const uint64_t cki = (uint64_t)f * a.n_ck * a.max_chunks + j + (uint64_t)(ag ? ag - 1u : 0u) * a.max_chunks;
   const uint32_t i_first = ag == 0u ? 0u : a.ev_ck[cki];
   unsigned long long q = a.chunk_start[base + j] + (ag == 0u ? 0ull : (a.ck[cki] >> 32));

@@ -3067,6 +3067,8 @@ __global__ __launch_bounds__(PK_THREADS, PACK_BLOCKS_PER_CU) void enc_pack(EncAr
       wbase += (i < wid) ? ws : 0u;
       gbits += ws;
     }
+    // (waves ranked by their bits at priorities 3..0 for the puts: no
+    // faster, r06zv_ab_pack_place.log)
     PROF_MARK(1);
     const bool over = gbits > a.pack_cap_bits;   // block-uniform
 #ifndef NICE_PACK_LATE_AGG
